@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- MSamples/s of the batched uniformly-partitioned convolver.
+
+Workload (BASELINE.json configs[1], the north-star metric's config): 1024
+channels per GPU, block 256, a distinct 48,000-tap white-noise IR per channel,
+f32.  One *step* = one FFTConvolver::process call of 256 samples on every
+channel (src/fft_convolver.rs:229-309) = one fused kernel launch: forward R2C
+of the new block into the FDL, the S-segment spectral MAC, C2R and overlap-add.
+Inputs are resident in HBM when the timed region starts.
+
+Multi-GPU (BASELINE configs[3], 8192 channels on 8 GPUs): one process per GPU,
+1024 channels per rank (weak scaling, channel shards have no data-path
+exchange); barrier + synchronize around the timed region, max time over ranks.
+`--dry shared` instead broadcasts one dry block per step from rank 0 over RCCL
+(the "one source, many IRs" case) and feeds it to every channel.
+
+Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused
+kernel and `cpu_baseline` from the oracle port on this host (rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fft-convolution_amd"))
+
+METRIC = "MSamples/s convolved (block=256, IR=48000) per node; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes_per_channel_block(B: int, L: int) -> int:
+    """16*S*K (IR spectra + FDL read once) + 8*K (new X write)
+    + 4B (in) + 4B (out) + 8B (overlap r/w), K = B+1 bins, S = ceil(L/B).
+    cfg2: 779,208 B."""
+    S = -(-L // B)
+    K = B + 1
+    return 16 * S * K + 8 * K + 4 * B + 4 * B + 8 * B
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--channels", type=int, default=1024, help="channels per GPU")
+    p.add_argument("--block", type=int, default=256)
+    p.add_argument("--ir", type=int, default=48000)
+    p.add_argument("--dry", choices=["per-channel", "shared"], default="per-channel")
+    p.add_argument("--ring", type=int, default=32, help="distinct input/output blocks kept in HBM")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU time per baseline leg")
+    p.add_argument("--traffic", default="", help="JSON file with PMC traffic (profiles/*pmc*.json) to attach")
+    return p.parse_args()
+
+
+def make_irs(rank: int, C: int, L: int) -> np.ndarray:
+    """Distinct IR per global channel: U[-1,1)/sqrt(L), seed 1234 + channel."""
+    out = np.empty((C, L), np.float32)
+    scale = 1.0 / np.sqrt(L)
+    for c in range(C):
+        g = np.random.default_rng(1234 + rank * C + c)
+        out[c] = g.uniform(-1.0, 1.0, L) * scale
+    return out
+
+
+def cpu_baseline(B: int, L: int, target_s: float):
+    """Oracle port timed on this host: 1 thread and all threads of this job."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the checker / CPU baseline only
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16, os.cpu_count() or 1))
+    res = {}
+    for th in sorted({1, threads}):
+        ch = 8 * th
+        t = oracle.bench_uniform(ch, B, L, 4, 1, th)  # calibration
+        per_block = max(t / 4, 1e-6)
+        nb = int(max(8, min(100000, target_s / per_block)))
+        secs = oracle.bench_uniform(ch, B, L, nb, 2, th)
+        res[th] = (ch * B * nb / secs / 1e6, ch, nb, secs)
+    v1 = res[1]
+    vt = res[threads]
+    return {
+        "value": round(vt[0], 3),
+        "unit": "MSamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle/fftconv_oracle.c FFTConvolver, B={B}, IR={L}: {vt[1]} channels x {vt[2]} blocks on "
+                   f"{threads} threads in {vt[3]:.1f}s; single thread {v1[1]} ch x {v1[2]} blocks = "
+                   f"{v1[0]:.3f} MSamples/s"),
+        "single_core_value": round(v1[0], 3),
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and world > 1:
+        args.gpus = world
+
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    import fftconv_amd as F
+
+    C, B, L = args.channels, args.block, args.ir
+    irs = make_irs(rank, C, L)
+    conv = F.FFTConvolver.init(irs, B, L, channels=C, device=local_rank)
+    del irs
+    S = conv.seg_count
+    ring = max(1, args.ring)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + rank)
+    if args.dry == "shared":
+        dry = torch.empty((ring, B), device=dev)
+        if rank == 0:
+            dry.uniform_(-1.0, 1.0, generator=g)
+        xin = None
+    else:
+        xin = torch.empty((ring, C, B), device=dev).uniform_(-1.0, 1.0, generator=g)
+    yout = torch.empty((ring, C, B), device=dev)
+    # a dedicated stream: torch's default stream is the NULL handle, which the
+    # C ABI reads as "the handle's own stream"
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sh = stream.cuda_stream
+    torch.cuda.synchronize(dev)
+
+    def step(i: int):
+        r = i % ring
+        if args.dry == "shared":
+            d = dry[r]
+            if dist is not None:
+                dist.broadcast(d, src=0)
+            # every channel reads the same broadcast block (input stride 0)
+            conv.process_device(d.data_ptr(), 0, yout[r].data_ptr(), B, B, sh)
+        else:
+            conv.process_device(xin[r].data_ptr(), B, yout[r].data_ptr(), B, B, sh)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1)  # HIP events on the launch stream
+    elapsed = max(wall, kern_ms / 1000.0)
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if not torch.isfinite(yout).all():
+        raise SystemExit("non-finite output")
+
+    total_samples = args.gpus * C * B * args.steps
+    value = total_samples / elapsed / 1e6
+    per_launch_s = kern_ms / 1000.0 / args.steps
+    bytes_per_launch = algorithmic_bytes_per_channel_block(B, L) * C
+    achieved = bytes_per_launch / per_launch_s / 1e9
+    traffic = None
+    if args.traffic and os.path.exists(args.traffic):
+        try:
+            traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if args.gpus == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(B, L, args.cpu_seconds)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "MSamples/s",
+            "n_gpus": args.gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1000.0 / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: white-noise U[-1,1) dry blocks resident in HBM, distinct white-noise IR "
+                    "U[-1,1)/sqrt(L) per channel",
+            "config": {
+                "workload": "cfg2 FFTConvolver batch" if args.gpus == 1 else "cfg4 FFTConvolver channel shards",
+                "channels_per_gpu": C,
+                "channels_total": C * args.gpus,
+                "block_size": B,
+                "ir_len": L,
+                "segments": S,
+                "dry_input": args.dry,
+                "parallelism": f"channel-shard x{args.gpus}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "upols_process_kernel<8,256>",
+                "bytes_per_launch": bytes_per_launch,
+                "launch_us": round(per_launch_s * 1e6, 3),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,942 @@
+// host.cpp -- C++ host side of the MI355X convolver and its C ABI (include/fftconv.h).
+//
+// The three reference types are mirrored as batches of device-resident
+// channels:
+//   UniformCore   <- FFTConvolver          (src/fft_convolver.rs:100-321)
+//   TwoStageCore  <- TwoStageFFTConvolver  (src/fft_convolver.rs:337-526)
+//   CrossfadeCore <- CrossfadeConvolver<FFTConvolver> (src/crossfade_convolver.rs:3-105)
+// Per-channel block state lives on the device (the fused kernel advances it);
+// the host only keeps what the reference keeps per *instance* and what all
+// channels share in lockstep (two-stage fill/position, the crossfader).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/fftconv.h"
+#include "kernels.hpp"
+
+using namespace fftconv;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const std::string &m) { g_last_error = m; }
+
+struct Status {
+    int code = FFTCONV_OK;
+    explicit operator bool() const { return code != FFTCONV_OK; }
+};
+
+int fail(int code, const std::string &m) {
+    set_error(m);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e__ = (expr);                                                         \
+        if (e__ != hipSuccess)                                                           \
+            return fail(FFTCONV_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e__)); \
+    } while (0)
+
+size_t next_pow2(size_t v) {  // usize::next_power_of_two (0 -> 1)
+    size_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+int ilog2(size_t v) {
+    int l = 0;
+    while (((size_t)1 << l) < v) ++l;
+    return l;
+}
+size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }  // == (a as f64 / b as f64).ceil()
+
+template <class T>
+struct DevPtr {
+    T *p = nullptr;
+    size_t n = 0;
+    DevPtr() = default;
+    DevPtr(const DevPtr &) = delete;
+    DevPtr &operator=(const DevPtr &) = delete;
+    ~DevPtr() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    int alloc(size_t count) {
+        reset();
+        n = count;
+        if (count == 0) return FFTCONV_OK;
+        hipError_t e = hipMalloc((void **)&p, count * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            n = 0;
+            return fail(e == hipErrorOutOfMemory ? FFTCONV_E_NOMEM : FFTCONV_E_DEVICE,
+                        std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+        return FFTCONV_OK;
+    }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int now = -1;
+        (void)hipGetDevice(&now);
+        if (prev >= 0 && now != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int check_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(FFTCONV_E_DEVICE, "no HIP device available (the convolver has no CPU fallback)");
+    if (device < 0 || device >= n) return fail(FFTCONV_E_DEVICE, "device index out of range");
+    return FFTCONV_OK;
+}
+
+// Device scratch for the host-pointer entry points (grown on demand).
+struct Scratch {
+    DevPtr<float> in, out;
+    int ensure(size_t nin, size_t nout) {
+        if (in.n < nin) { if (int r = in.alloc(nin)) return r; }
+        if (out.n < nout) { if (int r = out.alloc(nout)) return r; }
+        return FFTCONV_OK;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// UniformCore -- a batch of FFTConvolver instances
+// ---------------------------------------------------------------------------
+struct UniformCore {
+    int device = 0;
+    size_t C = 0;         // channels
+    size_t ir_len = 0;    // max_response_length (padded IR length)
+    size_t B = 0;         // block_size.next_power_of_two()
+    int log2b = 0;
+    size_t S = 0;         // seg_count
+    DevPtr<float2> H, X, pre, tw;
+    DevPtr<float> overlap, inbuf, staging;
+    DevPtr<int4> state;
+    hipStream_t stream = nullptr;
+    Scratch scratch;
+
+    ~UniformCore() {
+        if (stream) {
+            DeviceGuard g(device);
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+    }
+
+    int alloc_geometry(int dev, size_t channels, size_t max_block_size, size_t max_len) {
+        device = dev;
+        C = channels;
+        ir_len = max_len;
+        B = next_pow2(max_block_size);                             // :129
+        log2b = ilog2(B);
+        if (log2b > kMaxLog2Block)
+            return fail(FFTCONV_E_UNSUPPORTED, "block size " + std::to_string(B) + " exceeds 8192");
+        S = ceil_div(ir_len, B);                                   // :131
+        if (S * B > (size_t)INT32_MAX || C > (size_t)INT32_MAX)
+            return fail(FFTCONV_E_UNSUPPORTED, "geometry exceeds 32-bit indexing");
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        if (int r = H.alloc(C * S * B)) return r;
+        if (int r = X.alloc(C * S * B)) return r;
+        if (int r = pre.alloc(C * B)) return r;
+        if (int r = overlap.alloc(C * B)) return r;
+        if (int r = inbuf.alloc(C * B)) return r;
+        if (int r = state.alloc(C)) return r;
+        if (int r = tw.alloc(2 * B)) return r;
+        if (int r = staging.alloc(C * ir_len)) return r;  // update() never allocates
+        // twiddles W_N^k in double, rounded to f32
+        std::vector<float2> t(2 * B);
+        const size_t N = 2 * B;
+        for (size_t k = 0; k < N; ++k) {
+            const double ang = -2.0 * M_PI * (double)k / (double)N;
+            t[k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+        }
+        HIP_TRY(hipMemcpy(tw.p, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
+        return FFTCONV_OK;
+    }
+
+    // fresh state: zero FDL/overlap/buffers, {current 0, active S, fill 0}
+    int zero_state() {
+        if (X.n) HIP_TRY(hipMemsetAsync(X.p, 0, X.bytes(), stream));
+        if (pre.n) HIP_TRY(hipMemsetAsync(pre.p, 0, pre.bytes(), stream));
+        if (overlap.n) HIP_TRY(hipMemsetAsync(overlap.p, 0, overlap.bytes(), stream));
+        if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), stream));
+        std::vector<int4> st(C, make_int4(0, (int)S, 0, 0));
+        if (C) HIP_TRY(hipMemcpyAsync(state.p, st.data(), C * sizeof(int4), hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    // run the IR partition FFT from device samples (channel c at src + c*stride)
+    int ir_from_device(size_t chan0, size_t nch, const float *src, size_t stride, size_t len_data,
+                       size_t len_active, bool update_state, hipStream_t s) {
+        IrArgs a{};
+        a.H = H.p; a.overlap = overlap.p; a.pre = pre.p; a.state = state.p;
+        a.src = src; a.src_stride = (long long)stride;
+        a.len_data = (long long)len_data; a.len_active = (long long)len_active;
+        a.tw = tw.p; a.S = (int)S; a.chan0 = (int)chan0; a.update_state = update_state ? 1 : 0;
+        HIP_TRY(launch_ir_segments(log2b, a, (int)nch, s));
+        return FFTCONV_OK;
+    }
+
+    // upload host IRs (channel c at src + c*stride, len samples) into staging rows
+    int upload(size_t chan0, size_t nch, const float *src, size_t len, size_t stride, hipStream_t s) {
+        if (len == 0 || nch == 0) return FFTCONV_OK;
+        float *dst = staging.p + chan0 * ir_len;
+        if (stride == 0 || nch == 1) {
+            HIP_TRY(hipMemcpyAsync(dst, src, len * sizeof(float), hipMemcpyHostToDevice, s));
+        } else {
+            HIP_TRY(hipMemcpy2DAsync(dst, ir_len * sizeof(float), src, stride * sizeof(float),
+                                     len * sizeof(float), nch, hipMemcpyHostToDevice, s));
+        }
+        return FFTCONV_OK;
+    }
+
+    int init(int dev, size_t channels, const float *responses, size_t len, size_t stride, size_t max_block,
+             size_t max_len) {
+        if (max_len < len)                                          // :120-124
+            return fail(FFTCONV_E_INVALID,
+                        "max_response_length must be at least the length of the initial impulse response");
+        if (int r = check_device(dev)) return r;
+        DeviceGuard g(dev);
+        if (int r = alloc_geometry(dev, channels, max_block, max_len)) return r;
+        if (int r = zero_state()) return r;
+        if (S > 0) {
+            if (int r = upload(0, C, responses, len, stride == 0 ? 0 : stride, stream)) return r;
+            // every channel reads its own staging row; a shared response reads row 0
+            const size_t sst = (stride == 0 && C > 1) ? 0 : ir_len;
+            if (int r = ir_from_device(0, C, staging.p, sst, len, ir_len, false, stream)) return r;
+        }
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    // FFTConvolver::update (:188-227) for channels [chan0, chan0+nch)
+    int update_host(size_t chan0, size_t nch, const float *src, size_t len, size_t stride) {
+        if (len > ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
+        if (ir_len == 0) return FFTCONV_OK;                        // :195-197
+        DeviceGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());  // work may be in flight on a caller stream
+        if (int r = upload(chan0, nch, src, len, stride, stream)) return r;
+        const size_t sst = (stride == 0 && nch > 1) ? 0 : ir_len;
+        if (int r = ir_from_device(chan0, nch, staging.p + chan0 * ir_len, sst, len, len, true, stream)) return r;
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    // update() from device samples, stream-ordered (used by the crossfade swap)
+    int update_device(const float *src, size_t stride, size_t len, hipStream_t s) {
+        if (len > ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
+        if (ir_len == 0) return FFTCONV_OK;
+        return ir_from_device(0, C, src, stride, len, len, true, s);
+    }
+
+    int reset(hipStream_t s) {  // :310-320
+        if (X.n) HIP_TRY(hipMemsetAsync(X.p, 0, X.bytes(), s));
+        if (overlap.n) HIP_TRY(hipMemsetAsync(overlap.p, 0, overlap.bytes(), s));
+        if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), s));
+        if (pre.n) HIP_TRY(hipMemsetAsync(pre.p, 0, pre.bytes(), s));
+        HIP_TRY(launch_reset_state(state.p, (int)C, s));
+        return FFTCONV_OK;
+    }
+
+    int process_device(const float *din, size_t is, float *dout, size_t os, size_t n, hipStream_t s) {
+        if (n > (size_t)INT32_MAX) return fail(FFTCONV_E_UNSUPPORTED, "process length exceeds 2^31-1");
+        if (n == 0 || C == 0) return FFTCONV_OK;
+        ProcArgs a{};
+        a.H = H.p; a.X = X.p; a.overlap = overlap.p; a.inbuf = inbuf.p; a.pre = pre.p; a.state = state.p;
+        a.in = din; a.in_stride = (long long)is; a.out = dout; a.out_stride = (long long)os;
+        a.tw = tw.p; a.S = (int)S; a.n = (int)n;
+        HIP_TRY(launch_process(log2b, a, (int)C, s));
+        return FFTCONV_OK;
+    }
+
+    int process_host(const float *in, size_t in_len, float *out, size_t out_len) {
+        if (in_len < out_len) return fail(FFTCONV_E_INVALID, "input slice shorter than output (range end index out of range)");
+        if (out_len == 0 || C == 0) return FFTCONV_OK;
+        DeviceGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        if (int r = scratch.ensure(C * out_len, C * out_len)) return r;
+        HIP_TRY(hipMemcpy2DAsync(scratch.in.p, out_len * sizeof(float), in, in_len * sizeof(float),
+                                 out_len * sizeof(float), C, hipMemcpyHostToDevice, stream));
+        if (int r = process_device(scratch.in.p, out_len, scratch.out.p, out_len, out_len, stream)) return r;
+        HIP_TRY(hipMemcpyAsync(out, scratch.out.p, C * out_len * sizeof(float), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    // #[derive(Clone)]
+    int clone_from(const UniformCore &o) {
+        DeviceGuard g(o.device);
+        HIP_TRY(hipDeviceSynchronize());
+        device = o.device;
+        C = o.C; ir_len = o.ir_len; B = o.B; log2b = o.log2b; S = o.S;
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        auto cp = [&](auto &dst, const auto &src) -> int {
+            if (int r = dst.alloc(src.n)) return r;
+            if (src.n) HIP_TRY(hipMemcpyAsync(dst.p, src.p, src.bytes(), hipMemcpyDeviceToDevice, stream));
+            return FFTCONV_OK;
+        };
+        if (int r = cp(H, o.H)) return r;
+        if (int r = cp(X, o.X)) return r;
+        if (int r = cp(pre, o.pre)) return r;
+        if (int r = cp(tw, o.tw)) return r;
+        if (int r = cp(overlap, o.overlap)) return r;
+        if (int r = cp(inbuf, o.inbuf)) return r;
+        if (int r = cp(state, o.state)) return r;
+        if (int r = staging.alloc(o.staging.n)) return r;
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    int channel_state(size_t c, size_t out3[3]) {
+        if (c >= C) return fail(FFTCONV_E_INVALID, "channel out of range");
+        DeviceGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        int4 st;
+        HIP_TRY(hipMemcpy(&st, state.p + c, sizeof(int4), hipMemcpyDeviceToHost));
+        out3[0] = (size_t)st.x; out3[1] = (size_t)st.y; out3[2] = (size_t)st.z;
+        return FFTCONV_OK;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// TwoStageCore -- TwoStageFFTConvolver (src/fft_convolver.rs:337-526)
+// ---------------------------------------------------------------------------
+struct TwoStageCore {
+    int device = 0;
+    size_t C = 0, head_bs = 0, T = 0;
+    std::unique_ptr<UniformCore> head, tail0, tail;  // null tail = Default (zeros)
+    DevPtr<float> out0, pre0, out1, pre1, tin;      // [C][T] each
+    float *tail_output0 = nullptr, *tail_precalculated0 = nullptr;
+    float *tail_output = nullptr, *tail_precalculated = nullptr;
+    size_t tail_input_fill = 0, precalculated_pos = 0;
+    hipStream_t stream = nullptr;
+    Scratch scratch;
+
+    ~TwoStageCore() {
+        if (stream) {
+            DeviceGuard g(device);
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+    }
+
+    int alloc_buffers() {
+        for (auto *b : {&out0, &pre0, &out1, &pre1, &tin}) {
+            if (int r = b->alloc(C * T)) return r;
+            if (b->n) HIP_TRY(hipMemsetAsync(b->p, 0, b->bytes(), stream));
+        }
+        tail_output0 = out0.p; tail_precalculated0 = pre0.p;
+        tail_output = out1.p; tail_precalculated = pre1.p;
+        return FFTCONV_OK;
+    }
+
+    int init(int dev, size_t channels, const float *responses, size_t len, size_t stride, size_t block_size,
+             size_t max_len) {
+        head_bs = block_size;                                                   // :355
+        T = fftconv_compute_tail_block_size(block_size, max_len);              // :356
+        if (max_len < len)                                                      // :358-362
+            return fail(FFTCONV_E_INVALID,
+                        "max_response_length must be at least the length of the initial impulse response");
+        if (int r = check_device(dev)) return r;
+        if (ilog2(T) > kMaxLog2Block)
+            return fail(FFTCONV_E_UNSUPPORTED, "tail block size " + std::to_string(T) + " exceeds 8192");
+        device = dev;
+        C = channels;
+        DeviceGuard g(dev);
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        // padded_ir = response zero-extended to max_len (:363-364); sub-ranges
+        // are cut on the host so each stage sees exactly its reference slice
+        const size_t sstride = stride == 0 ? 0 : stride;
+        auto slice = [&](size_t off, size_t cnt, std::vector<float> &buf) -> size_t {
+            // rows of `cnt` samples starting at padded_ir[off]; returns the row stride used
+            const size_t rows = (sstride == 0) ? 1 : C;
+            buf.assign(rows * std::max<size_t>(cnt, 1), 0.f);
+            for (size_t c = 0; c < rows; ++c)
+                for (size_t j = 0; j < cnt; ++j) {
+                    const size_t p = off + j;
+                    buf[c * cnt + j] = p < len ? responses[c * sstride + p] : 0.f;
+                }
+            return sstride == 0 ? 0 : cnt;
+        };
+        std::vector<float> tmp;
+        const size_t head_ir_len = std::min(max_len, T);                        // :366-368
+        head.reset(new (std::nothrow) UniformCore());
+        if (!head) return fail(FFTCONV_E_NOMEM, "out of host memory");
+        size_t st = slice(0, head_ir_len, tmp);
+        if (int r = head->init(dev, C, tmp.data(), head_ir_len, st, head_bs, head_ir_len)) return r;
+        if (max_len > T) {                                                      // :370-382
+            const size_t tl = std::min(max_len - T, T);
+            tail0.reset(new (std::nothrow) UniformCore());
+            if (!tail0) return fail(FFTCONV_E_NOMEM, "out of host memory");
+            st = slice(T, tl, tmp);
+            if (int r = tail0->init(dev, C, tmp.data(), tl, st, head_bs, tl)) return r;
+        }
+        if (max_len > 2 * T) {                                                  // :387-398
+            const size_t tl = max_len - 2 * T;
+            tail.reset(new (std::nothrow) UniformCore());
+            if (!tail) return fail(FFTCONV_E_NOMEM, "out of host memory");
+            st = slice(2 * T, tl, tmp);
+            if (int r = tail->init(dev, C, tmp.data(), tl, st, T, tl)) return r;
+        }
+        if (int r = alloc_buffers()) return r;
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    // TwoStageFFTConvolver::process (:426-509)
+    int process_device(const float *din, size_t is, float *dout, size_t os, size_t len, hipStream_t s) {
+        if (len > head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
+        if (int r = head->process_device(din, is, dout, os, len, s)) return r;   // :431
+        size_t processed = 0;
+        while (processed < len) {                                                 // :441
+            const size_t processing = std::min(len - processed, head_bs - (tail_input_fill % head_bs));
+            if (tail_input_fill + processing > T)  // tail_input[fill..fill+processing] out of range (:473-474)
+                return fail(FFTCONV_E_INVALID, "range end index out of range for slice of length tail_block_size");
+            TwoStageAccumArgs a{};
+            a.out = dout; a.out_stride = (long long)os;
+            a.p0 = tail_precalculated0; a.p1 = tail_precalculated; a.T = (long long)T;
+            a.pos = (int)precalculated_pos; a.in = din; a.in_stride = (long long)is;
+            a.sb = (int)processed; a.tail_input = tin.p; a.fill = (int)tail_input_fill; a.cnt = (int)processing;
+            HIP_TRY(launch_twostage_accum(a, (int)C, s));                        // :452-475
+            precalculated_pos += processing;
+            tail_input_fill += processing;
+            if (tail_input_fill % head_bs == 0) {                                 // :478-490
+                const size_t off = tail_input_fill - head_bs;
+                if (tail0) {
+                    if (int r = tail0->process_device(tin.p + off, T, tail_output0 + off, T, head_bs, s)) return r;
+                }
+                if (tail_input_fill == T) std::swap(tail_precalculated0, tail_output0);
+            }
+            if (tail_input_fill == T) {                                           // :493-500
+                std::swap(tail_precalculated, tail_output);
+                if (tail) {
+                    if (int r = tail->process_device(tin.p, T, tail_output, T, T, s)) return r;
+                }
+            }
+            if (tail_input_fill == T) {                                           // :502-505
+                tail_input_fill = 0;
+                precalculated_pos = 0;
+            }
+            processed += processing;
+        }
+        return FFTCONV_OK;
+    }
+
+    int process_host(const float *in, float *out, size_t len) {
+        if (len > head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
+        if (len == 0 || C == 0) return FFTCONV_OK;
+        DeviceGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        if (int r = scratch.ensure(C * len, C * len)) return r;
+        HIP_TRY(hipMemcpyAsync(scratch.in.p, in, C * len * sizeof(float), hipMemcpyHostToDevice, stream));
+        if (int r = process_device(scratch.in.p, len, scratch.out.p, len, len, stream)) return r;
+        HIP_TRY(hipMemcpyAsync(out, scratch.out.p, C * len * sizeof(float), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    int reset() {  // :511-525
+        DeviceGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        if (int r = head->reset(stream)) return r;
+        if (tail0) { if (int r = tail0->reset(stream)) return r; }
+        if (tail) { if (int r = tail->reset(stream)) return r; }
+        for (auto *b : {&out0, &pre0, &out1, &pre1, &tin})
+            if (b->n) HIP_TRY(hipMemsetAsync(b->p, 0, b->bytes(), stream));
+        tail_input_fill = 0;
+        precalculated_pos = 0;
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    int clone_from(const TwoStageCore &o) {
+        DeviceGuard g(o.device);
+        HIP_TRY(hipDeviceSynchronize());
+        device = o.device; C = o.C; head_bs = o.head_bs; T = o.T;
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        auto cl = [&](std::unique_ptr<UniformCore> &dst, const std::unique_ptr<UniformCore> &src) -> int {
+            if (!src) return FFTCONV_OK;
+            dst.reset(new (std::nothrow) UniformCore());
+            if (!dst) return fail(FFTCONV_E_NOMEM, "out of host memory");
+            return dst->clone_from(*src);
+        };
+        if (int r = cl(head, o.head)) return r;
+        if (int r = cl(tail0, o.tail0)) return r;
+        if (int r = cl(tail, o.tail)) return r;
+        if (int r = alloc_buffers()) return r;
+        auto map = [&](const float *p) -> float * {  // same role, this instance's buffer
+            if (p == o.out0.p) return out0.p;
+            if (p == o.pre0.p) return pre0.p;
+            if (p == o.out1.p) return out1.p;
+            return pre1.p;
+        };
+        tail_output0 = map(o.tail_output0); tail_precalculated0 = map(o.tail_precalculated0);
+        tail_output = map(o.tail_output); tail_precalculated = map(o.tail_precalculated);
+        const std::pair<DevPtr<float> *, const DevPtr<float> *> pairs[] = {
+            {&out0, &o.out0}, {&pre0, &o.pre0}, {&out1, &o.out1}, {&pre1, &o.pre1}, {&tin, &o.tin}};
+        for (auto &pr : pairs)
+            if (pr.second->n)
+                HIP_TRY(hipMemcpyAsync(pr.first->p, pr.second->p, pr.second->bytes(), hipMemcpyDeviceToDevice, stream));
+        tail_input_fill = o.tail_input_fill;
+        precalculated_pos = o.precalculated_pos;
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Crossfader<RaisedCosineMixer> host state (src/crossfade_convolver.rs:192-279);
+// the per-sample gains are evaluated on the device by crossfade_mix_kernel.
+// ---------------------------------------------------------------------------
+struct Crossfader {
+    int64_t fading_samples = 0, hold_samples = 0, counter = 0;
+    float mix_value_step = 0.f, mix_value = 0.f;
+    bool approaching = false;
+    int target = 0;  // 0 = A, 1 = B
+
+    void init(size_t fading, size_t hold) {  // :204-214
+        fading_samples = (int64_t)fading;
+        hold_samples = (int64_t)hold;
+        counter = 0;
+        mix_value_step = 1.0f / (float)fading;
+        mix_value = 0.f;
+        approaching = false;
+        target = 0;
+    }
+    void fade_into(int t) {  // :216-240
+        if (target == t) return;
+        if (!approaching) {
+            counter = -hold_samples;
+            approaching = true;
+            target = t;
+            mix_value_step = -mix_value_step;
+        } else if (counter >= 0) {
+            counter = fading_samples - counter;
+            target = t;
+            mix_value_step = -mix_value_step;
+        } else {
+            approaching = false;
+            target = t;
+        }
+    }
+    // advance the state machine over n samples exactly as n calls of mix() (:242-278)
+    void advance(size_t n) {
+        for (size_t i = 0; i < n && approaching; ++i) {
+            counter += 1;
+            if (counter <= 0) continue;
+            volatile float v = mix_value + mix_value_step;  // one f32 rounding per step
+            mix_value = v;
+            if (counter == fading_samples) {
+                approaching = false;
+                mix_value = target == 0 ? 0.0f : 1.0f;
+            }
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// CrossfadeCore -- CrossfadeConvolver<FFTConvolver> (src/crossfade_convolver.rs:3-105)
+// ---------------------------------------------------------------------------
+struct CrossfadeCore {
+    int device = 0;
+    size_t C = 0, max_buffer_size = 0, stored_len = 0, stored_stride = 0;
+    std::unique_ptr<UniformCore> a, b;
+    Crossfader xf;
+    DevPtr<float> buf_a, buf_b, stored;
+    bool response_pending = false;
+    hipStream_t stream = nullptr;
+    Scratch scratch;
+
+    ~CrossfadeCore() {
+        if (stream) {
+            DeviceGuard g(device);
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+    }
+
+    // CrossfadeConvolver::new (:19-43)
+    int init_new(const UniformCore &conv, size_t max_response_length, size_t mbs, size_t crossfade_samples) {
+        device = conv.device;
+        C = conv.C;
+        DeviceGuard g(device);
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        a.reset(new (std::nothrow) UniformCore());
+        b.reset(new (std::nothrow) UniformCore());
+        if (!a || !b) return fail(FFTCONV_E_NOMEM, "out of host memory");
+        if (int r = a->clone_from(conv)) return r;
+        if (int r = b->clone_from(conv)) return r;
+        stored_len = max_response_length;
+        stored_stride = stored_len;
+        if (int r = stored.alloc(C * stored_len)) return r;
+        if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), stream));
+        xf.init(crossfade_samples, std::min(mbs, max_response_length));
+        max_buffer_size = mbs;
+        if (int r = buf_a.alloc(C * mbs)) return r;
+        if (int r = buf_b.alloc(C * mbs)) return r;
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    bool is_crossfading() const { return xf.approaching; }  // :85-92
+
+    // swap (:94-105) from device samples
+    int swap_device(const float *src, size_t stride, size_t len, hipStream_t s) {
+        if (xf.target == 0) {
+            if (int r = b->update_device(src, stride, len, s)) return r;
+            xf.fade_into(1);
+        } else {
+            if (int r = a->update_device(src, stride, len, s)) return r;
+            xf.fade_into(0);
+        }
+        return FFTCONV_OK;
+    }
+
+    // Convolution::update (:51-64); host samples, channel c at src + c*stride (stride 0 = shared)
+    int update_host(const float *src, size_t len, size_t stride) {
+        DeviceGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        if (!is_crossfading()) {
+            UniformCore &t = xf.target == 0 ? *b : *a;
+            if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
+            if (int r = t.update_host(0, C, src, len, stride)) return r;
+            xf.fade_into(xf.target == 0 ? 1 : 0);
+            response_pending = false;
+            return FFTCONV_OK;
+        }
+        if (len > stored_len) return fail(FFTCONV_E_INVALID, "assertion failed: response_len <= self.stored_response.len()");
+        // stored_response[..len] = response; stored_response[len..] = 0
+        if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), stream));
+        if (len) {
+            if (stride == 0 || C == 1) {
+                HIP_TRY(hipMemcpyAsync(stored.p, src, len * sizeof(float), hipMemcpyHostToDevice, stream));
+                stored_stride = C == 1 ? stored_len : 0;
+            } else {
+                HIP_TRY(hipMemcpy2DAsync(stored.p, stored_len * sizeof(float), src, stride * sizeof(float),
+                                         len * sizeof(float), C, hipMemcpyHostToDevice, stream));
+                stored_stride = stored_len;
+            }
+        }
+        HIP_TRY(hipStreamSynchronize(stream));
+        response_pending = true;
+        return FFTCONV_OK;
+    }
+
+    // Convolution::process (:66-78)
+    int process_device(const float *din, size_t is, float *dout, size_t os, size_t out_len, hipStream_t s) {
+        if (out_len > max_buffer_size) return fail(FFTCONV_E_INVALID, "output longer than max_buffer_size (index out of bounds)");
+        if (!is_crossfading() && response_pending) {                    // :67-70
+            if (int r = swap_device(stored.p, stored_stride, stored_len, s)) return r;
+            response_pending = false;
+        }
+        const size_t m = max_buffer_size;
+        if (int r = a->process_device(din, is, buf_a.p, m, m, s)) return r;   // :72
+        if (int r = b->process_device(din, is, buf_b.p, m, m, s)) return r;   // :73
+        CrossfadeMixArgs x{};
+        x.buf_a = buf_a.p; x.buf_b = buf_b.p; x.buf_stride = (long long)m;
+        x.out = dout; x.out_stride = (long long)os; x.n = (int)out_len;
+        x.approaching = xf.approaching ? 1 : 0; x.target = xf.target;
+        x.counter0 = xf.counter; x.fading = xf.fading_samples;
+        x.mix_value0 = xf.mix_value; x.step = xf.mix_value_step;
+        HIP_TRY(launch_crossfade_mix(x, (int)C, s));                      // :75-77
+        xf.advance(out_len);
+        return FFTCONV_OK;
+    }
+
+    int process_host(const float *in, size_t in_len, float *out, size_t out_len) {
+        if (in_len < max_buffer_size) return fail(FFTCONV_E_INVALID, "input shorter than max_buffer_size (range end index out of range)");
+        if (out_len > max_buffer_size) return fail(FFTCONV_E_INVALID, "output longer than max_buffer_size (index out of bounds)");
+        if (C == 0) return FFTCONV_OK;
+        DeviceGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        const size_t m = max_buffer_size;
+        if (int r = scratch.ensure(C * m, C * std::max<size_t>(out_len, 1))) return r;
+        if (m)
+            HIP_TRY(hipMemcpy2DAsync(scratch.in.p, m * sizeof(float), in, in_len * sizeof(float), m * sizeof(float), C,
+                                     hipMemcpyHostToDevice, stream));
+        if (int r = process_device(scratch.in.p, m, scratch.out.p, std::max<size_t>(out_len, 1), out_len, stream)) return r;
+        if (out_len)
+            HIP_TRY(hipMemcpy2DAsync(out, out_len * sizeof(float), scratch.out.p, out_len * sizeof(float),
+                                     out_len * sizeof(float), C, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    int clone_from(const CrossfadeCore &o) {
+        DeviceGuard g(o.device);
+        HIP_TRY(hipDeviceSynchronize());
+        device = o.device; C = o.C; max_buffer_size = o.max_buffer_size;
+        stored_len = o.stored_len; stored_stride = o.stored_stride;
+        xf = o.xf; response_pending = o.response_pending;
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        a.reset(new (std::nothrow) UniformCore());
+        b.reset(new (std::nothrow) UniformCore());
+        if (!a || !b) return fail(FFTCONV_E_NOMEM, "out of host memory");
+        if (int r = a->clone_from(*o.a)) return r;
+        if (int r = b->clone_from(*o.b)) return r;
+        if (int r = buf_a.alloc(o.buf_a.n)) return r;
+        if (int r = buf_b.alloc(o.buf_b.n)) return r;
+        if (int r = stored.alloc(o.stored.n)) return r;
+        if (stored.n) HIP_TRY(hipMemcpyAsync(stored.p, o.stored.p, stored.bytes(), hipMemcpyDeviceToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+};
+
+template <class T>
+T *make_or_null(int r, T *p) {
+    if (r != FFTCONV_OK) {
+        delete p;
+        return nullptr;
+    }
+    return p;
+}
+
+hipStream_t pick(void *s, hipStream_t own) { return s ? (hipStream_t)s : own; }
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+struct fftconv_uniform { UniformCore core; };
+struct fftconv_twostage { TwoStageCore core; };
+struct fftconv_crossfade { CrossfadeCore core; };
+
+extern "C" {
+
+int fftconv_abi_version(void) { return FFTCONV_ABI_VERSION; }
+const char *fftconv_last_error(void) { return g_last_error.c_str(); }
+int fftconv_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+size_t fftconv_complex_size(size_t size) { return size / 2 + 1; }
+
+// compute_tail_block_size, src/fft_convolver.rs:528-540, in f32 exactly as written
+size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
+    const volatile float FFT_K = 1.5f;
+    const volatile float ln2 = logf(2.0f);
+    volatile float kn = (FFT_K * (float)head_len);
+    kn = kn / (2.0f * ln2);
+    volatile float kk = kn * kn;
+    volatile float lh = (float)response_len * (float)head_len;
+    volatile float sum = kk + lh;
+    volatile float b = -kn + sqrtf(sum);
+    const float h = (float)head_len;
+    float bb = (b != b) ? h : (b > h ? b : h);
+    size_t bi;
+    if (!(bb > 0.0f)) bi = 0;
+    else if (bb >= 18446744073709551615.0f) bi = SIZE_MAX;
+    else bi = (size_t)bb;
+    return next_pow2(bi);
+}
+
+// ---- uniform --------------------------------------------------------------
+fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len, size_t max_block_size,
+                                      size_t max_response_length) {
+    return fftconv_uniform_init_batch(0, 1, response, response_len, response_len, max_block_size,
+                                      max_response_length);
+}
+
+fftconv_uniform *fftconv_uniform_init_batch(int device, size_t channels, const float *responses,
+                                            size_t response_len, size_t response_stride, size_t max_block_size,
+                                            size_t max_response_length) {
+    set_error("");
+    auto *h = new (std::nothrow) fftconv_uniform();
+    if (!h) { set_error("out of host memory"); return nullptr; }
+    int r = h->core.init(device, channels, responses, response_len, response_stride, max_block_size,
+                         max_response_length);
+    return make_or_null(r, h);
+}
+
+int fftconv_uniform_update(fftconv_uniform *h, const float *response, size_t len) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.update_host(0, h->core.C, response, len, 0);
+}
+int fftconv_uniform_update_batch(fftconv_uniform *h, const float *responses, size_t len, size_t stride) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.update_host(0, h->core.C, responses, len, h->core.C == 1 ? 0 : stride);
+}
+int fftconv_uniform_update_channel(fftconv_uniform *h, size_t channel, const float *response, size_t len) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    if (channel >= h->core.C) return fail(FFTCONV_E_INVALID, "channel out of range");
+    return h->core.update_host(channel, 1, response, len, 0);
+}
+int fftconv_uniform_reset(fftconv_uniform *h) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    HIP_TRY(hipDeviceSynchronize());
+    if (int r = h->core.reset(h->core.stream)) return r;
+    HIP_TRY(hipStreamSynchronize(h->core.stream));
+    return FFTCONV_OK;
+}
+int fftconv_uniform_process(fftconv_uniform *h, const float *input, size_t input_len, float *output,
+                            size_t output_len) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.process_host(input, input_len, output, output_len);
+}
+int fftconv_uniform_process_device(fftconv_uniform *h, const float *d_input, size_t in_stride, float *d_output,
+                                   size_t out_stride, size_t len, void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    return h->core.process_device(d_input, in_stride, d_output, out_stride, len, pick(hip_stream, h->core.stream));
+}
+fftconv_uniform *fftconv_uniform_clone(const fftconv_uniform *h) {
+    if (!h) { set_error("null handle"); return nullptr; }
+    auto *c = new (std::nothrow) fftconv_uniform();
+    if (!c) { set_error("out of host memory"); return nullptr; }
+    return make_or_null(c->core.clone_from(h->core), c);
+}
+void fftconv_uniform_destroy(fftconv_uniform *h) { delete h; }
+int fftconv_uniform_synchronize(fftconv_uniform *h) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    HIP_TRY(hipStreamSynchronize(h->core.stream));
+    return FFTCONV_OK;
+}
+size_t fftconv_uniform_channels(const fftconv_uniform *h) { return h ? h->core.C : 0; }
+size_t fftconv_uniform_block_size(const fftconv_uniform *h) { return h ? h->core.B : 0; }
+size_t fftconv_uniform_seg_count(const fftconv_uniform *h) { return h ? h->core.S : 0; }
+int fftconv_uniform_channel_state(const fftconv_uniform *h, size_t channel, size_t out3[3]) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return const_cast<UniformCore &>(h->core).channel_state(channel, out3);
+}
+
+// ---- two-stage ------------------------------------------------------------
+fftconv_twostage *fftconv_twostage_init(const float *response, size_t response_len, size_t max_block_size,
+                                        size_t max_response_length) {
+    return fftconv_twostage_init_batch(0, 1, response, response_len, response_len, max_block_size,
+                                       max_response_length);
+}
+fftconv_twostage *fftconv_twostage_init_batch(int device, size_t channels, const float *responses,
+                                              size_t response_len, size_t response_stride, size_t max_block_size,
+                                              size_t max_response_length) {
+    set_error("");
+    auto *h = new (std::nothrow) fftconv_twostage();
+    if (!h) { set_error("out of host memory"); return nullptr; }
+    int r = h->core.init(device, channels, responses, response_len, channels == 1 ? response_len : response_stride,
+                         max_block_size, max_response_length);
+    return make_or_null(r, h);
+}
+int fftconv_twostage_update(fftconv_twostage *h, const float *, size_t) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return fail(FFTCONV_E_UNIMPLEMENTED, "not yet implemented (TwoStageFFTConvolver::update is todo!())");
+}
+int fftconv_twostage_reset(fftconv_twostage *h) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.reset();
+}
+int fftconv_twostage_process(fftconv_twostage *h, const float *input, float *output, size_t len) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.process_host(input, output, len);
+}
+int fftconv_twostage_process_device(fftconv_twostage *h, const float *d_input, size_t in_stride, float *d_output,
+                                    size_t out_stride, size_t len, void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    return h->core.process_device(d_input, in_stride, d_output, out_stride, len, pick(hip_stream, h->core.stream));
+}
+fftconv_twostage *fftconv_twostage_clone(const fftconv_twostage *h) {
+    if (!h) { set_error("null handle"); return nullptr; }
+    auto *c = new (std::nothrow) fftconv_twostage();
+    if (!c) { set_error("out of host memory"); return nullptr; }
+    return make_or_null(c->core.clone_from(h->core), c);
+}
+void fftconv_twostage_destroy(fftconv_twostage *h) { delete h; }
+int fftconv_twostage_synchronize(fftconv_twostage *h) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    HIP_TRY(hipStreamSynchronize(h->core.stream));
+    return FFTCONV_OK;
+}
+size_t fftconv_twostage_tail_block_size(const fftconv_twostage *h) { return h ? h->core.T : 0; }
+
+// ---- crossfade ------------------------------------------------------------
+fftconv_crossfade *fftconv_crossfade_init(const float *response, size_t response_len, size_t max_block_size,
+                                          size_t max_response_length) {
+    return fftconv_crossfade_init_batch(0, 1, response, response_len, response_len, max_block_size,
+                                        max_response_length);
+}
+fftconv_crossfade *fftconv_crossfade_init_batch(int device, size_t channels, const float *responses,
+                                                size_t response_len, size_t response_stride, size_t max_block_size,
+                                                size_t max_response_length) {
+    set_error("");
+    fftconv_uniform *conv = fftconv_uniform_init_batch(device, channels, responses, response_len, response_stride,
+                                                       max_block_size, max_response_length);
+    if (!conv) return nullptr;
+    // Convolution::init (src/crossfade_convolver.rs:46-49)
+    fftconv_crossfade *h = fftconv_crossfade_new(conv, response_len, max_block_size, response_len);
+    fftconv_uniform_destroy(conv);
+    return h;
+}
+fftconv_crossfade *fftconv_crossfade_new(const fftconv_uniform *convolver, size_t max_response_length,
+                                         size_t max_buffer_size, size_t crossfade_samples) {
+    if (!convolver) { set_error("null handle"); return nullptr; }
+    auto *h = new (std::nothrow) fftconv_crossfade();
+    if (!h) { set_error("out of host memory"); return nullptr; }
+    int r = h->core.init_new(convolver->core, max_response_length, max_buffer_size, crossfade_samples);
+    return make_or_null(r, h);
+}
+int fftconv_crossfade_update(fftconv_crossfade *h, const float *response, size_t len) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.update_host(response, len, 0);
+}
+int fftconv_crossfade_update_batch(fftconv_crossfade *h, const float *responses, size_t len, size_t stride) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.update_host(responses, len, h->core.C == 1 ? 0 : stride);
+}
+int fftconv_crossfade_reset(fftconv_crossfade *h) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return fail(FFTCONV_E_UNIMPLEMENTED, "not yet implemented (CrossfadeConvolver::reset is todo!())");
+}
+int fftconv_crossfade_process(fftconv_crossfade *h, const float *input, size_t input_len, float *output,
+                              size_t output_len) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return h->core.process_host(input, input_len, output, output_len);
+}
+int fftconv_crossfade_process_device(fftconv_crossfade *h, const float *d_input, size_t in_stride, float *d_output,
+                                     size_t out_stride, size_t output_len, void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    return h->core.process_device(d_input, in_stride, d_output, out_stride, output_len,
+                                  pick(hip_stream, h->core.stream));
+}
+int fftconv_crossfade_is_crossfading(const fftconv_crossfade *h) { return h && h->core.is_crossfading() ? 1 : 0; }
+fftconv_crossfade *fftconv_crossfade_clone(const fftconv_crossfade *h) {
+    if (!h) { set_error("null handle"); return nullptr; }
+    auto *c = new (std::nothrow) fftconv_crossfade();
+    if (!c) { set_error("out of host memory"); return nullptr; }
+    return make_or_null(c->core.clone_from(h->core), c);
+}
+void fftconv_crossfade_destroy(fftconv_crossfade *h) { delete h; }
+int fftconv_crossfade_synchronize(fftconv_crossfade *h) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    HIP_TRY(hipStreamSynchronize(h->core.stream));
+    return FFTCONV_OK;
+}
+
+}  // extern "C"

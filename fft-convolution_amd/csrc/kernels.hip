@@ -1,0 +1,492 @@
+// kernels.hip -- gfx950 kernels of the batched partitioned convolver.
+//
+// One workgroup owns one channel (one reference FFTConvolver instance) for
+// the whole call, so every piece of per-channel state stays private to a CU
+// and no inter-workgroup protocol is needed.
+//
+// HBM layout (per uniform batch: C channels, block B, S segments):
+//   H   float2 [C][S][B]  packed IR segment spectra      (segments_ir)
+//   X   float2 [C][S][B]  packed frequency-domain delay line (segments)
+//   ovl float  [C][B]     overlap                        (overlap)
+//   ib  float  [C][B]     input buffer, only touched for partial blocks
+//   pre float2 [C][B]     pre_multiplied, only touched for partial blocks
+//   st  int4   [C]        {current, active_seg_count, input_buffer_fill, flags}
+// A packed row is B complex = 8B bytes (slot 0 = (DC, Nyquist)), so each
+// channel's H and X are contiguous 8*S*B-byte streams read with 16-byte
+// loads (float4 = 2 bins per lane).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "fft_lds.hpp"
+#include "kernels.hpp"
+
+namespace fftconv {
+
+// ---------------------------------------------------------------------------
+// Geometry of the fused step kernel for a given block size
+// ---------------------------------------------------------------------------
+template <int LOG2B, int NT>
+struct Geo {
+    static constexpr int B = 1 << LOG2B;
+    static constexpr int VEC = B >= 2 ? 2 : 1;          // complex bins per lane-slot
+    static constexpr int F = B / VEC;                   // slots per row
+    static constexpr int G = F >= NT ? 1 : NT / F;      // row groups (segment split)
+    static constexpr int SPT = F >= NT ? F / NT : 1;    // slots per thread
+    static constexpr int U = SPT >= 8 ? 1 : 8 / SPT;    // rows in flight per thread
+    static constexpr size_t red_bytes = G > 1 ? (size_t)NT * VEC * sizeof(float2) : 0;
+    static constexpr size_t lds_bytes = 2 * (size_t)B * sizeof(float2) + red_bytes + 16;
+};
+
+template <int VEC> struct VecT;
+template <> struct VecT<2> { using type = float4; };
+template <> struct VecT<1> { using type = float2; };
+
+// Complex multiply-accumulate over one lane-slot, complex_multiply_accumulate
+// (src/fft_convolver.rs:76-88) for 2 bins.  dc/ny carry the products of the
+// packed real bins so that slot 0 can be resolved as (DC, Nyquist).
+struct Acc2 {
+    float4 a;
+    float dc, ny;
+    __device__ __forceinline__ void zero() { a = make_float4(0.f, 0.f, 0.f, 0.f); dc = ny = 0.f; }
+    __device__ __forceinline__ void mac(float4 h, float4 x) {
+        a.x += h.x * x.x - h.y * x.y;
+        a.y += h.x * x.y + h.y * x.x;
+        a.z += h.z * x.z - h.w * x.w;
+        a.w += h.z * x.w + h.w * x.z;
+        dc += h.x * x.x;
+        ny += h.y * x.y;
+    }
+    __device__ __forceinline__ float4 get(int slot) const {
+        return slot == 0 ? make_float4(dc, ny, a.z, a.w) : a;
+    }
+};
+struct Acc1 {  // B == 1: the only bin pair is (DC, Nyquist)
+    float2 a;
+    __device__ __forceinline__ void zero() { a = make_float2(0.f, 0.f); }
+    __device__ __forceinline__ void mac(float2 h, float2 x) { a.x += h.x * x.x; a.y += h.y * x.y; }
+    __device__ __forceinline__ float2 get(int) const { return a; }
+};
+template <int VEC> using AccT = std::conditional_t<VEC == 2, Acc2, Acc1>;
+
+__device__ __forceinline__ float4 vadd(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+
+// conv = pre + x (.) h for one slot, packed-aware (slot 0 bin 0 is (DC, Nyquist)).
+__device__ __forceinline__ float4 slot_mac(float4 pre, float4 x, float4 h, int slot) {
+    float4 r;
+    if (slot == 0) {
+        r.x = pre.x + x.x * h.x;
+        r.y = pre.y + x.y * h.y;
+    } else {
+        r.x = pre.x + (x.x * h.x - x.y * h.y);
+        r.y = pre.y + (x.x * h.y + x.y * h.x);
+    }
+    r.z = pre.z + (x.z * h.z - x.w * h.w);
+    r.w = pre.w + (x.z * h.w + x.w * h.z);
+    return r;
+}
+__device__ __forceinline__ float2 slot_mac(float2 pre, float2 x, float2 h, int) {
+    return make_float2(pre.x + x.x * h.x, pre.y + x.y * h.y);
+}
+__device__ __forceinline__ bool slot0_finite(float4 v) { return isfinite(v.x) && isfinite(v.y); }
+__device__ __forceinline__ bool slot0_finite(float2 v) { return isfinite(v.x) && isfinite(v.y); }
+
+// ---------------------------------------------------------------------------
+// Fused UPOLS step: FFTConvolver::process (src/fft_convolver.rs:229-309) for
+// one channel per workgroup, the whole chunk loop of one call on device.
+// ---------------------------------------------------------------------------
+template <int LOG2B, int NT>
+__global__ __launch_bounds__(NT) void upols_process_kernel(ProcArgs a) {
+    using Gm = Geo<LOG2B, NT>;
+    constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT, U = Gm::U;
+    constexpr float invN = 1.0f / (float)(2 * B);
+    using vec_t = typename VecT<VEC>::type;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *bufA = reinterpret_cast<float2 *>(smem);
+    float2 *bufB = bufA + B;
+    vec_t *red = reinterpret_cast<vec_t *>(bufB + B);
+    int &s_err = *reinterpret_cast<int *>(smem + 2 * (size_t)B * sizeof(float2) + Gm::red_bytes);
+
+    const int tid = threadIdx.x;
+    const size_t c = blockIdx.x;
+    const int4 st = a.state[c];
+    int cur = st.x;
+    const int act = st.y;
+    int fill = st.z;
+    int flags = st.w;
+    float *outc = a.out + c * a.out_stride;
+    const float *inc = a.in + c * a.in_stride;
+    const int n = a.n;
+
+    if (act == 0) {  // :230-233 -- zero output, state untouched
+        for (int j = tid; j < n; j += NT) outc[j] = 0.f;
+        return;
+    }
+
+    const size_t rows = (size_t)a.S * B;
+    const float2 *Hc = a.H + c * rows;
+    float2 *Xc = a.X + c * rows;
+    float *ovc = a.overlap + c * B;
+    float *ibc = a.inbuf + c * B;
+    float2 *prec = a.pre + c * B;
+    const float2 *__restrict__ tw = a.tw;
+
+    // slot ownership: the MAC splits rows over G groups; the owner of slot f
+    // after the reduction is thread f (G > 1) or thread f % NT (G == 1).
+    const int f0 = G > 1 ? tid % F : tid;
+    const int g = G > 1 ? tid / F : 0;
+    const bool owner = G > 1 ? tid < F : true;
+
+    vec_t pacc[SPT];
+    if (fill != 0 && owner) {  // a partial block carries pre_multiplied over
+#pragma unroll
+        for (int s = 0; s < SPT; ++s) pacc[s] = reinterpret_cast<const vec_t *>(prec)[f0 + s * NT];
+    }
+
+    int processed = 0;
+    bool err = false;
+    while (processed < n) {
+        const bool was_empty = fill == 0;                               // :237
+        const int k = min(n - processed, B - fill);                      // :238-241
+
+        if (was_empty) {                                                 // :258-269
+            AccT<VEC> acc[SPT];
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) acc[s].zero();
+            int i = 1 + g;
+            int xi = act > 0 ? (cur + i) % act : 0;  // index_audio = (current + i) % active
+            for (; i + (U - 1) * G < act; i += U * G) {
+                vec_t hv[U][SPT], xv[U][SPT];
+                int xr = xi;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)(i + u * G) * B);
+                    const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xr * B);
+#pragma unroll
+                    for (int s = 0; s < SPT; ++s) {
+                        hv[u][s] = hrow[f0 + s * NT];
+                        xv[u][s] = xrow[f0 + s * NT];
+                    }
+                    xr += G;
+                    if (xr >= act) xr -= act;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int s = 0; s < SPT; ++s) acc[s].mac(hv[u][s], xv[u][s]);
+                xi = xr;
+            }
+            for (; i < act; i += G) {
+                const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)i * B);
+                const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xi * B);
+#pragma unroll
+                for (int s = 0; s < SPT; ++s)
+                    acc[s].mac(hrow[f0 + s * NT],
+                               xrow[f0 + s * NT]);
+                xi += G;
+                if (xi >= act) xi -= act;
+            }
+            if constexpr (G > 1) {
+                red[g * F + f0] = acc[0].get(f0);
+                __syncthreads();
+                if (owner) {
+                    vec_t p = red[f0];
+#pragma unroll
+                    for (int q = 1; q < G; ++q) p = vadd(p, red[q * F + f0]);
+                    pacc[0] = p;
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) pacc[s] = acc[s].get(f0 + s * NT);
+            }
+        }
+
+        // forward FFT of the zero-padded input buffer into segments[current]
+        // (:243-255): x[i] = chunk sample, else the carried input buffer.
+        for (int m = tid; m < B; m += NT) {
+            float2 z = make_float2(0.f, 0.f);
+            const int i0 = 2 * m, i1 = 2 * m + 1;
+            if (i0 < B) {
+                z.x = (i0 >= fill && i0 < fill + k) ? inc[processed + i0 - fill]
+                                                     : ((flags & FLAG_INBUF) ? ibc[i0] : 0.f);
+            }
+            if (i1 < B) {
+                z.y = (i1 >= fill && i1 < fill + k) ? inc[processed + i1 - fill]
+                                                     : ((flags & FLAG_INBUF) ? ibc[i1] : 0.f);
+            }
+            bufA[m] = z;
+        }
+        if (tid == 0) s_err = 0;
+        __syncthreads();
+        float2 *Z = lds_cfft<LOG2B, NT, false>(bufA, bufB, tw);
+        float2 *Q = Z == bufA ? bufB : bufA;
+        float2 *Xcur = Xc + (size_t)cur * B;
+        for (int m = tid; m < B; m += NT) {
+            const float2 v = real_post<LOG2B, NT>(Z, m, tw);
+            Q[m] = v;
+            Xcur[m] = v;
+        }
+        __syncthreads();
+
+        // conv = pre_multiplied + segments[current] (.) segments_ir[0] (:270-275)
+        if (owner) {
+            const vec_t *h0 = reinterpret_cast<const vec_t *>(Hc);
+            const vec_t *q = reinterpret_cast<const vec_t *>(Q);
+            vec_t *zc = reinterpret_cast<vec_t *>(Z);
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+                const int f = f0 + s * NT;
+                const vec_t cv = slot_mac(pacc[s], q[f], h0[f], f);
+                zc[f] = cv;
+                // realfft's C2R rejects a non-zero DC/Nyquist imaginary part,
+                // which only a non-finite operand can produce (:278-281)
+                if (f == 0 && !slot0_finite(cv)) s_err = 1;
+            }
+        }
+        __syncthreads();
+        if (s_err) { err = true; break; }
+
+        // inverse FFT (:278) with the 1/N of Fft::inverse (:58-60)
+        for (int m = tid; m < B; m += NT) Q[m] = real_pre<LOG2B, NT>(Z, m, tw);
+        __syncthreads();
+        float2 *Y = lds_cfft<LOG2B, NT, true>(Q, Z, tw);
+        const float *y = reinterpret_cast<const float *>(Y);
+
+        // overlap-add (:284-288)
+        for (int j = tid; j < k; j += NT) outc[processed + j] = y[fill + j] * invN + ovc[fill + j];
+        const bool complete = fill + k == B;                              // :291-292
+        if (complete) {
+            __syncthreads();
+            for (int j = tid; j < B; j += NT) ovc[j] = y[B + j] * invN;  // :297-298
+            if (flags & FLAG_INBUF)
+                for (int j = tid; j < B; j += NT) ibc[j] = 0.f;           // :294
+            flags &= ~FLAG_INBUF;
+            fill = 0;
+            cur = cur > 0 ? cur - 1 : act - 1;                            // :301-305
+        } else {
+            for (int j = tid; j < k; j += NT) ibc[fill + j] = inc[processed + j];
+            flags |= FLAG_INBUF;
+            fill += k;
+        }
+        processed += k;
+        __syncthreads();
+    }
+
+    if (err) {
+        // output.fill(0); return -- state stays at the failing chunk: its
+        // input is in the buffer, fill and current unchanged.
+        const int k = min(n - processed, B - fill);
+        for (int j = tid; j < k; j += NT) ibc[fill + j] = inc[processed + j];
+        flags |= FLAG_INBUF;
+        for (int j = tid; j < n; j += NT) outc[j] = 0.f;
+    }
+    if ((fill != 0 || err) && owner) {
+#pragma unroll
+        for (int s = 0; s < SPT; ++s) reinterpret_cast<vec_t *>(prec)[f0 + s * NT] = pacc[s];
+    }
+    if (tid == 0) a.state[c] = make_int4(cur, act, fill, flags);
+}
+
+// ---------------------------------------------------------------------------
+// IR partition: FFTConvolver::init (:145-156) / update (:204-226).
+// grid (S, channels): workgroup (i, c) transforms segment i of channel
+// chan0 + c; segments at or past ceil(len_active / B) are zeroed.
+// ---------------------------------------------------------------------------
+template <int LOG2B, int NT>
+__global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
+    constexpr int B = 1 << LOG2B;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *bufA = reinterpret_cast<float2 *>(smem);
+    float2 *bufB = bufA + B;
+    const int tid = threadIdx.x;
+    const int i = blockIdx.x;
+    const size_t c = a.chan0 + blockIdx.y;
+    const size_t rows = (size_t)a.S * B;
+    float2 *row = a.H + c * rows + (size_t)i * B;
+    const long long active = (a.len_active + B - 1) / B;
+
+    if (a.update_state && i == 0) {
+        // update(): zero overlap / pre_multiplied / conv, set active (:199-204)
+        for (int j = tid; j < B; j += NT) {
+            a.overlap[c * B + j] = 0.f;
+            a.pre[c * B + j] = make_float2(0.f, 0.f);
+        }
+        if (tid == 0) a.state[c].y = (int)active;
+    }
+    if (i >= active) {  // :224-226
+        for (int j = tid; j < B; j += NT) row[j] = make_float2(0.f, 0.f);
+        return;
+    }
+    const float *src = a.src + blockIdx.y * a.src_stride;
+    const long long base = (long long)i * B;
+    for (int m = tid; m < B; m += NT) {
+        const long long i0 = base + 2 * m, i1 = base + 2 * m + 1;
+        float2 z;
+        z.x = (2 * m < B && i0 < a.len_data) ? src[i0] : 0.f;
+        z.y = (2 * m + 1 < B && i1 < a.len_data) ? src[i1] : 0.f;
+        bufA[m] = z;
+    }
+    __syncthreads();
+    const float2 *Z = lds_cfft<LOG2B, NT, false>(bufA, bufB, a.tw);
+    for (int m = tid; m < B; m += NT) row[m] = real_post<LOG2B, NT>(Z, m, a.tw);
+}
+
+// ---------------------------------------------------------------------------
+// TwoStage sub-chunk (src/fft_convolver.rs:452-475): output += precalculated0
+// then += precalculated (two passes, like the reference), and append the
+// input to tail_input.
+// ---------------------------------------------------------------------------
+__global__ void twostage_accum_kernel(TwoStageAccumArgs a) {
+    const size_t c = blockIdx.x;
+    float *o = a.out + c * a.out_stride + a.sb;
+    const float *p0 = a.p0 + c * a.T + a.pos;
+    const float *p1 = a.p1 + c * a.T + a.pos;
+    const float *x = a.in + c * a.in_stride + a.sb;
+    float *ti = a.tail_input + c * a.T + a.fill;
+    for (int j = threadIdx.x; j < a.cnt; j += blockDim.x) {
+        float v = o[j];
+        v += p0[j];
+        v += p1[j];
+        o[j] = v;
+        ti[j] = x[j];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Crossfade mix (src/crossfade_convolver.rs:75-77 + Crossfader::mix :242-278
+// + RaisedCosineMixer :160-169), all channels in lockstep.  Each sample
+// recomputes its mix_value by the same sequential f32 additions the
+// reference performs, so the gains are bit-identical to a serial walk.
+// ---------------------------------------------------------------------------
+__global__ void crossfade_mix_kernel(CrossfadeMixArgs a) {
+    const size_t c = blockIdx.x;
+    const float *A = a.buf_a + c * a.buf_stride;
+    const float *Bv = a.buf_b + c * a.buf_stride;
+    float *o = a.out + c * a.out_stride;
+    const float PI_HALF = 3.14159265358979323846f * 0.5f;
+    for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
+        const float va = A[j], vb = Bv[j];
+        float r;
+        if (!a.approaching) {
+            r = a.target == 0 ? va : vb;
+        } else {
+            const long long cj = a.counter0 + j + 1;
+            if (cj <= 0) {
+                r = a.target == 0 ? vb : va;                // hold the previous target
+            } else if (a.fading >= 1 && cj >= a.fading) {
+                r = a.target == 0 ? va : vb;                // reached (snap)
+            } else {
+                const long long inc = cj - (a.counter0 > 0 ? a.counter0 : 0);
+                float v = a.mix_value0;
+                for (long long q = 0; q < inc; ++q) v = __fadd_rn(v, a.step);
+                const float rad = __fmul_rn(PI_HALF, v);
+                const float cs = cosf(rad);
+                const float g1 = __fmul_rn(cs, cs);
+                const float g2 = __fsub_rn(1.0f, g1);
+                r = __fadd_rn(__fmul_rn(va, g1), __fmul_rn(vb, g2));
+            }
+        }
+        o[j] = r;
+    }
+}
+
+// FFTConvolver::reset (src/fft_convolver.rs:310-320) scalar part: current = 0,
+// input_buffer_fill = 0; active_seg_count is kept.
+__global__ void reset_state_kernel(int4 *state, int channels) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < channels) {
+        int4 s = state[c];
+        state[c] = make_int4(0, s.y, 0, 0);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+constexpr int kNT = 256;
+
+template <int LOG2B>
+static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t s) {
+    using Gm = Geo<LOG2B, kNT>;
+    auto kern = upols_process_kernel<LOG2B, kNT>;
+    if (Gm::lds_bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)Gm::lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(channels), dim3(kNT), Gm::lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+template <int LOG2B>
+static hipError_t launch_ir_t(const IrArgs &a, int channels, hipStream_t s) {
+    constexpr size_t lds = 2 * (size_t)(1 << LOG2B) * sizeof(float2) + 16;
+    auto kern = ir_segments_kernel<LOG2B, kNT>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(a.S, channels), dim3(kNT), lds, s, a);
+    return hipGetLastError();
+}
+
+#define FFTCONV_DISPATCH(FN, LOG2B, ...)                      \
+    switch (LOG2B) {                                          \
+        case 0: return FN<0>(__VA_ARGS__);                    \
+        case 1: return FN<1>(__VA_ARGS__);                    \
+        case 2: return FN<2>(__VA_ARGS__);                    \
+        case 3: return FN<3>(__VA_ARGS__);                    \
+        case 4: return FN<4>(__VA_ARGS__);                    \
+        case 5: return FN<5>(__VA_ARGS__);                    \
+        case 6: return FN<6>(__VA_ARGS__);                    \
+        case 7: return FN<7>(__VA_ARGS__);                    \
+        case 8: return FN<8>(__VA_ARGS__);                    \
+        case 9: return FN<9>(__VA_ARGS__);                    \
+        case 10: return FN<10>(__VA_ARGS__);                  \
+        case 11: return FN<11>(__VA_ARGS__);                  \
+        case 12: return FN<12>(__VA_ARGS__);                  \
+        case 13: return FN<13>(__VA_ARGS__);                  \
+        default: return hipErrorInvalidValue;                 \
+    }
+
+hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    FFTCONV_DISPATCH(launch_process_t, log2b, a, channels, s)
+}
+
+hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s) {
+    if (channels <= 0 || a.S <= 0) return hipSuccess;
+    FFTCONV_DISPATCH(launch_ir_t, log2b, a, channels, s)
+}
+
+hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipStream_t s) {
+    if (channels <= 0 || a.cnt <= 0) return hipSuccess;
+    hipLaunchKernelGGL(twostage_accum_kernel, dim3(channels), dim3(a.cnt >= 256 ? 256 : 64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStream_t s) {
+    if (channels <= 0 || a.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(crossfade_mix_kernel, dim3(channels), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    hipLaunchKernelGGL(reset_state_kernel, dim3((channels + 255) / 256), dim3(256), 0, s, state, channels);
+    return hipGetLastError();
+}
+
+size_t process_lds_bytes(int log2b) {
+    switch (log2b) {
+#define LDSCASE(L) case L: return Geo<L, kNT>::lds_bytes;
+        LDSCASE(0) LDSCASE(1) LDSCASE(2) LDSCASE(3) LDSCASE(4) LDSCASE(5) LDSCASE(6)
+        LDSCASE(7) LDSCASE(8) LDSCASE(9) LDSCASE(10) LDSCASE(11) LDSCASE(12) LDSCASE(13)
+#undef LDSCASE
+        default: return 0;
+    }
+}
+
+}  // namespace fftconv

@@ -1,0 +1,80 @@
+// kernels.hpp -- host-visible kernel argument blocks and launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace fftconv {
+
+enum : int { FLAG_INBUF = 1 };  // the HBM input buffer holds live samples
+
+struct ProcArgs {
+    const float2 *H;       // [C][S][B] packed IR spectra
+    float2 *X;             // [C][S][B] packed FDL
+    float *overlap;        // [C][B]
+    float *inbuf;          // [C][B]
+    float2 *pre;           // [C][B]
+    int4 *state;           // [C] {current, active, fill, flags}
+    const float *in;
+    long long in_stride;
+    float *out;
+    long long out_stride;
+    const float2 *tw;      // W_N^k, k < N = 2B
+    int S;                 // seg_count (row pitch of H and X in rows)
+    int n;                 // output samples this call
+};
+
+struct IrArgs {
+    float2 *H;
+    float *overlap;
+    float2 *pre;
+    int4 *state;
+    const float *src;      // device IR samples of channel chan0 (+ src_stride per channel)
+    long long src_stride;
+    long long len_data;    // samples present in src
+    long long len_active;  // length that sets active_seg_count = ceil(len_active / B)
+    const float2 *tw;
+    int S;
+    int chan0;
+    int update_state;      // 1: update() side effects (zero overlap/pre, set active)
+};
+
+struct TwoStageAccumArgs {
+    float *out;
+    long long out_stride;
+    const float *p0;       // tail_precalculated0 [C][T]
+    const float *p1;       // tail_precalculated  [C][T]
+    long long T;
+    int pos;               // precalculated_pos
+    const float *in;
+    long long in_stride;
+    int sb;                // sub-chunk start within the call
+    float *tail_input;     // [C][T]
+    int fill;              // tail_input_fill before the append
+    int cnt;               // samples in the sub-chunk
+};
+
+struct CrossfadeMixArgs {
+    const float *buf_a;
+    const float *buf_b;
+    long long buf_stride;
+    float *out;
+    long long out_stride;
+    int n;
+    int approaching;       // FadingState::Approaching
+    int target;            // 0 = A, 1 = B
+    long long counter0;
+    long long fading;
+    float mix_value0;
+    float step;
+};
+
+hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_t s);
+hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s);
+hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipStream_t s);
+hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStream_t s);
+hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s);
+size_t process_lds_bytes(int log2b);
+
+constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)
+
+}  // namespace fftconv

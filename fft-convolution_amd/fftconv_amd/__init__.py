@@ -1,0 +1,345 @@
+"""fftconv_amd -- Python mirror of the reference's `Convolution` trait over the
+MI355X C ABI (include/fftconv.h, libfftconv_amd.so).
+
+    FFTConvolver.init(response, max_block_size, max_response_length)   src/fft_convolver.rs:119
+    .update(response) / .reset() / .process(input[, out_len]) / .clone()
+    TwoStageFFTConvolver.init(...)                                      src/fft_convolver.rs:354
+    CrossfadeConvolver.init(...) / CrossfadeConvolver.new(conv, ...)    src/crossfade_convolver.rs:19-49
+
+Every object is a batch of `channels` independent convolvers on one GPU
+(channels=1 is exactly one reference instance).  Host arrays are
+[channels][samples] (1-D for a single channel).  `process_device` takes raw
+device pointers (e.g. torch tensors' data_ptr()) and a HIP stream and is
+asynchronous.
+
+A reference panic surfaces as `ConvolutionPanic`; HIP failures as
+`DeviceError`.  There is no CPU fallback: importing works anywhere, but
+creating a convolver needs the HIP library and a gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libfftconv_amd.so")
+
+FFTCONV_OK = 0
+FFTCONV_E_INVALID = -1
+FFTCONV_E_UNIMPLEMENTED = -2
+FFTCONV_E_UNSUPPORTED = -3
+FFTCONV_E_DEVICE = -4
+FFTCONV_E_NOMEM = -5
+
+# every symbol include/fftconv.h declares: name -> (restype, argtypes)
+_vp, _sz, _fp, _i = C.c_void_p, C.c_size_t, C.POINTER(C.c_float), C.c_int
+SIGNATURES = {
+    "fftconv_abi_version": (_i, []),
+    "fftconv_last_error": (C.c_char_p, []),
+    "fftconv_device_count": (_i, []),
+    "fftconv_complex_size": (_sz, [_sz]),
+    "fftconv_compute_tail_block_size": (_sz, [_sz, _sz]),
+    "fftconv_uniform_init": (_vp, [_fp, _sz, _sz, _sz]),
+    "fftconv_uniform_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
+    "fftconv_uniform_update": (_i, [_vp, _fp, _sz]),
+    "fftconv_uniform_update_batch": (_i, [_vp, _fp, _sz, _sz]),
+    "fftconv_uniform_update_channel": (_i, [_vp, _sz, _fp, _sz]),
+    "fftconv_uniform_reset": (_i, [_vp]),
+    "fftconv_uniform_process": (_i, [_vp, _fp, _sz, _fp, _sz]),
+    "fftconv_uniform_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
+    "fftconv_uniform_clone": (_vp, [_vp]),
+    "fftconv_uniform_destroy": (None, [_vp]),
+    "fftconv_uniform_synchronize": (_i, [_vp]),
+    "fftconv_uniform_channels": (_sz, [_vp]),
+    "fftconv_uniform_block_size": (_sz, [_vp]),
+    "fftconv_uniform_seg_count": (_sz, [_vp]),
+    "fftconv_uniform_channel_state": (_i, [_vp, _sz, C.POINTER(_sz)]),
+    "fftconv_twostage_init": (_vp, [_fp, _sz, _sz, _sz]),
+    "fftconv_twostage_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
+    "fftconv_twostage_update": (_i, [_vp, _fp, _sz]),
+    "fftconv_twostage_reset": (_i, [_vp]),
+    "fftconv_twostage_process": (_i, [_vp, _fp, _fp, _sz]),
+    "fftconv_twostage_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
+    "fftconv_twostage_clone": (_vp, [_vp]),
+    "fftconv_twostage_destroy": (None, [_vp]),
+    "fftconv_twostage_synchronize": (_i, [_vp]),
+    "fftconv_twostage_tail_block_size": (_sz, [_vp]),
+    "fftconv_crossfade_init": (_vp, [_fp, _sz, _sz, _sz]),
+    "fftconv_crossfade_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
+    "fftconv_crossfade_new": (_vp, [_vp, _sz, _sz, _sz]),
+    "fftconv_crossfade_update": (_i, [_vp, _fp, _sz]),
+    "fftconv_crossfade_update_batch": (_i, [_vp, _fp, _sz, _sz]),
+    "fftconv_crossfade_reset": (_i, [_vp]),
+    "fftconv_crossfade_process": (_i, [_vp, _fp, _sz, _fp, _sz]),
+    "fftconv_crossfade_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
+    "fftconv_crossfade_is_crossfading": (_i, [_vp]),
+    "fftconv_crossfade_clone": (_vp, [_vp]),
+    "fftconv_crossfade_destroy": (None, [_vp]),
+    "fftconv_crossfade_synchronize": (_i, [_vp]),
+}
+
+
+class ConvolutionPanic(RuntimeError):
+    """Where the reference panics (assert!/panic!/slice bounds)."""
+
+
+class NotImplementedInReference(ConvolutionPanic):
+    """Where the reference has todo!()."""
+
+
+class DeviceError(RuntimeError):
+    """HIP runtime failure or no usable device."""
+
+
+_lib = None
+
+
+def lib():
+    """Load libfftconv_amd.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DeviceError(f"{LIB_PATH} not built -- run __graft_entry__.build() or make -C fft-convolution_amd")
+        # One HIP runtime per process: torch's libc10_hip loads its bundled
+        # libamdhip64 by the unversioned name, while this library NEEDs
+        # libamdhip64.so.7.  Loading torch first makes the dynamic linker bind
+        # our NEEDED entry to torch's copy (same SONAME), so device pointers and
+        # hipStream_t handles from torch are valid here; loading us first would
+        # put two HIP/HSA runtimes in the process and torch would see no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.fftconv_abi_version() != 1:
+            raise DeviceError("ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().fftconv_last_error().decode()
+
+
+def _check(rc: int):
+    if rc == FFTCONV_OK:
+        return
+    msg = last_error()
+    if rc == FFTCONV_E_INVALID:
+        raise ConvolutionPanic(msg)
+    if rc == FFTCONV_E_UNIMPLEMENTED:
+        raise NotImplementedInReference(msg)
+    raise DeviceError(f"status {rc}: {msg}")
+
+
+def _handle(h):
+    if not h:
+        msg = last_error()
+        if "max_response_length" in msg or "longer" in msg:
+            raise ConvolutionPanic(msg)
+        raise DeviceError(msg or "handle creation failed")
+    return h
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(_fp)
+
+
+def complex_size(n: int) -> int:
+    return int(lib().fftconv_complex_size(n))
+
+
+def compute_tail_block_size(head_len: int, response_len: int) -> int:
+    return int(lib().fftconv_compute_tail_block_size(head_len, response_len))
+
+
+def device_count() -> int:
+    return int(lib().fftconv_device_count())
+
+
+def _responses(responses, channels):
+    r = _f32(responses)
+    if r.ndim == 1:
+        return r, r.size, 0
+    if r.shape[0] != channels:
+        raise ValueError("responses must be [channels][len]")
+    return r, r.shape[1], r.shape[1]
+
+
+class _Base:
+    _prefix = ""
+
+    def __init__(self, h, channels: int):
+        self._h = h
+        self.channels = channels
+
+    def _fn(self, name):
+        return getattr(lib(), f"fftconv_{self._prefix}_{name}")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            getattr(_lib, f"fftconv_{self._prefix}_destroy")(h)
+            self._h = None
+
+    def _shape_in(self, x):
+        x = _f32(x)
+        if self.channels == 1 and x.ndim == 1:
+            return x, x.size, True
+        if x.ndim != 2 or x.shape[0] != self.channels:
+            raise ValueError(f"input must be [{self.channels}][n]")
+        return x, x.shape[1], False
+
+    def synchronize(self):
+        _check(self._fn("synchronize")(self._h))
+
+    def process_device(self, d_in: int, in_stride: int, d_out: int, out_stride: int, n: int, stream: int = 0):
+        _check(self._fn("process_device")(self._h, C.c_void_p(d_in), in_stride, C.c_void_p(d_out), out_stride, n,
+                                          C.c_void_p(stream) if stream else None))
+
+    def __copy__(self):
+        return self.clone()
+
+
+class FFTConvolver(_Base):
+    """FFTConvolver, src/fft_convolver.rs:100-321 (a batch of `channels`)."""
+
+    _prefix = "uniform"
+
+    @classmethod
+    def init(cls, response, max_block_size: int, max_response_length: int, *, channels: int = 1, device: int = 0):
+        r, n, stride = _responses(response, channels)
+        h = lib().fftconv_uniform_init_batch(device, channels, _p(r), n, stride, max_block_size, max_response_length)
+        return cls(_handle(h), channels)
+
+    def update(self, response):
+        r = _f32(response)
+        if r.ndim == 2:
+            _check(lib().fftconv_uniform_update_batch(self._h, _p(r), r.shape[1], r.shape[1]))
+        else:
+            _check(lib().fftconv_uniform_update(self._h, _p(r), r.size))
+
+    def update_channel(self, channel: int, response):
+        r = _f32(response)
+        _check(lib().fftconv_uniform_update_channel(self._h, channel, _p(r), r.size))
+
+    def reset(self):
+        _check(lib().fftconv_uniform_reset(self._h))
+
+    def process(self, inp, out_len: int | None = None) -> np.ndarray:
+        x, n_in, flat = self._shape_in(inp)
+        n = n_in if out_len is None else out_len
+        y = np.zeros((self.channels, n), np.float32)
+        _check(lib().fftconv_uniform_process(self._h, _p(x), n_in, _p(y), n))
+        return y[0] if flat else y
+
+    def clone(self):
+        return FFTConvolver(_handle(lib().fftconv_uniform_clone(self._h)), self.channels)
+
+    @property
+    def block_size(self) -> int:
+        return int(lib().fftconv_uniform_block_size(self._h))
+
+    @property
+    def seg_count(self) -> int:
+        return int(lib().fftconv_uniform_seg_count(self._h))
+
+    def channel_state(self, channel: int = 0):
+        """(current, active_seg_count, input_buffer_fill)."""
+        out = (C.c_size_t * 3)()
+        _check(lib().fftconv_uniform_channel_state(self._h, channel, out))
+        return tuple(int(v) for v in out)
+
+
+class TwoStageFFTConvolver(_Base):
+    """TwoStageFFTConvolver, src/fft_convolver.rs:337-526."""
+
+    _prefix = "twostage"
+
+    @classmethod
+    def init(cls, response, max_block_size: int, max_response_length: int, *, channels: int = 1, device: int = 0):
+        r, n, stride = _responses(response, channels)
+        h = lib().fftconv_twostage_init_batch(device, channels, _p(r), n, stride, max_block_size, max_response_length)
+        return cls(_handle(h), channels)
+
+    def update(self, response):
+        r = _f32(response)
+        _check(lib().fftconv_twostage_update(self._h, _p(r), r.size))
+
+    def reset(self):
+        _check(lib().fftconv_twostage_reset(self._h))
+
+    def process(self, inp) -> np.ndarray:
+        x, n, flat = self._shape_in(inp)
+        y = np.zeros((self.channels, n), np.float32)
+        _check(lib().fftconv_twostage_process(self._h, _p(x), _p(y), n))
+        return y[0] if flat else y
+
+    def clone(self):
+        return TwoStageFFTConvolver(_handle(lib().fftconv_twostage_clone(self._h)), self.channels)
+
+    @property
+    def tail_block_size(self) -> int:
+        return int(lib().fftconv_twostage_tail_block_size(self._h))
+
+
+class CrossfadeConvolver(_Base):
+    """CrossfadeConvolver<FFTConvolver>, src/crossfade_convolver.rs:3-105."""
+
+    _prefix = "crossfade"
+
+    def __init__(self, h, channels: int, max_buffer_size: int):
+        super().__init__(h, channels)
+        self.max_buffer_size = max_buffer_size
+
+    @classmethod
+    def init(cls, response, max_block_size: int, max_response_length: int, *, channels: int = 1, device: int = 0):
+        r, n, stride = _responses(response, channels)
+        h = lib().fftconv_crossfade_init_batch(device, channels, _p(r), n, stride, max_block_size, max_response_length)
+        return cls(_handle(h), channels, max_block_size)
+
+    @classmethod
+    def new(cls, convolver: FFTConvolver, max_response_length: int, max_buffer_size: int, crossfade_samples: int):
+        h = lib().fftconv_crossfade_new(convolver._h, max_response_length, max_buffer_size, crossfade_samples)
+        return cls(_handle(h), convolver.channels, max_buffer_size)
+
+    def update(self, response):
+        r = _f32(response)
+        if r.ndim == 2:
+            _check(lib().fftconv_crossfade_update_batch(self._h, _p(r), r.shape[1], r.shape[1]))
+        else:
+            _check(lib().fftconv_crossfade_update(self._h, _p(r), r.size))
+
+    def reset(self):
+        _check(lib().fftconv_crossfade_reset(self._h))
+
+    def process(self, inp, out_len: int | None = None) -> np.ndarray:
+        x, n_in, flat = self._shape_in(inp)
+        n = n_in if out_len is None else out_len
+        y = np.zeros((self.channels, n), np.float32)
+        _check(lib().fftconv_crossfade_process(self._h, _p(x), n_in, _p(y), n))
+        return y[0] if flat else y
+
+    def is_crossfading(self) -> bool:
+        return bool(lib().fftconv_crossfade_is_crossfading(self._h))
+
+    def clone(self):
+        return CrossfadeConvolver(_handle(lib().fftconv_crossfade_clone(self._h)), self.channels,
+                                  self.max_buffer_size)
+
+
+__all__ = [
+    "FFTConvolver", "TwoStageFFTConvolver", "CrossfadeConvolver", "ConvolutionPanic",
+    "NotImplementedInReference", "DeviceError", "complex_size", "compute_tail_block_size", "device_count",
+    "lib", "LIB_PATH", "SIGNATURES",
+]

@@ -1,0 +1,156 @@
+/*
+ * fftconv.h -- C ABI of the MI355X-native partitioned FFT convolver.
+ *
+ * Drop-in boundary for Sin-tel/fft-convolution's `Convolution` trait
+ * (src/lib.rs:5-14):
+ *
+ *     trait Convolution: Clone {
+ *         fn init(response: &[f32], max_block_size: usize, max_response_length: usize) -> Self;
+ *         fn update(&mut self, response: &[f32]);          // real-time safe
+ *         fn reset(&mut self);
+ *         fn process(&mut self, input: &[f32], output: &mut [f32]);
+ *     }
+ *
+ * Every handle is a *batch* of `channels` independent convolvers that share
+ * one geometry (block size, max response length) and live on one GPU.  A
+ * handle created by the single-channel `*_init` entry point is a batch of 1
+ * and is the exact counterpart of one reference instance.  Batched host
+ * buffers are laid out channel-major: sample j of channel c at [c*len + j]
+ * (or [c*stride + j] where a stride is taken).
+ *
+ * Errors: where the reference panics (assert!/panic!/todo!/slice bounds) the
+ * call returns a negative status and leaves the instance unchanged; the
+ * message is available from fftconv_last_error().  A runtime FFT error
+ * (realfft's C2R rejecting a non-finite DC/Nyquist bin) zero-fills that
+ * channel's output and leaves its block state where the reference leaves it
+ * (src/fft_convolver.rs:278-281); it is not an error status.
+ *
+ * There is no CPU fallback: creating a handle without a usable gfx950 device
+ * fails with FFTCONV_E_DEVICE.
+ */
+#ifndef FFTCONV_H
+#define FFTCONV_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FFTCONV_ABI_VERSION 1
+
+enum {
+    FFTCONV_OK = 0,
+    FFTCONV_E_INVALID = -1,       /* a reference panic!/assert!/slice-bounds precondition */
+    FFTCONV_E_UNIMPLEMENTED = -2, /* a reference todo!() */
+    FFTCONV_E_UNSUPPORTED = -3,   /* geometry outside this build (block size > 8192) */
+    FFTCONV_E_DEVICE = -4,        /* HIP runtime error / no device */
+    FFTCONV_E_NOMEM = -5
+};
+
+typedef struct fftconv_uniform fftconv_uniform;     /* FFTConvolver        src/fft_convolver.rs:100-321 */
+typedef struct fftconv_twostage fftconv_twostage;   /* TwoStageFFTConvolver src/fft_convolver.rs:337-526 */
+typedef struct fftconv_crossfade fftconv_crossfade; /* CrossfadeConvolver<FFTConvolver> src/crossfade_convolver.rs:10-105 */
+
+/* ---- library ----------------------------------------------------------- */
+int fftconv_abi_version(void);
+const char *fftconv_last_error(void);            /* thread-local, "" if none */
+int fftconv_device_count(void);                   /* visible HIP devices, 0 if none */
+size_t fftconv_complex_size(size_t size);         /* src/fft_convolver.rs:66-68 */
+size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /* :534-540 */
+
+/* ---- FFTConvolver (uniformly partitioned, zero latency) ---------------- */
+/* FFTConvolver::init, src/fft_convolver.rs:119-186.  NULL on error. */
+fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len,
+                                      size_t max_block_size, size_t max_response_length);
+/* Batched init on `device`: channel c's response is responses[c*response_stride ..
+ * + response_len] (host memory). */
+fftconv_uniform *fftconv_uniform_init_batch(int device, size_t channels, const float *responses,
+                                            size_t response_len, size_t response_stride,
+                                            size_t max_block_size, size_t max_response_length);
+/* FFTConvolver::update, src/fft_convolver.rs:188-227; every channel gets the
+ * same response.  No allocation (staging is reserved at init). */
+int fftconv_uniform_update(fftconv_uniform *h, const float *response, size_t response_len);
+/* Per-channel responses, host memory, channel c at responses[c*stride ..]. */
+int fftconv_uniform_update_batch(fftconv_uniform *h, const float *responses, size_t response_len,
+                                 size_t response_stride);
+/* One channel only. */
+int fftconv_uniform_update_channel(fftconv_uniform *h, size_t channel, const float *response,
+                                   size_t response_len);
+/* FFTConvolver::reset, src/fft_convolver.rs:310-320 (all channels). */
+int fftconv_uniform_reset(fftconv_uniform *h);
+/* FFTConvolver::process, src/fft_convolver.rs:229-309, host buffers:
+ * input [channels][input_len], output [channels][output_len]; reads
+ * input[0..output_len] of each channel (input_len >= output_len, else
+ * FFTCONV_E_INVALID like the reference's slice panic).  Synchronous. */
+int fftconv_uniform_process(fftconv_uniform *h, const float *input, size_t input_len,
+                            float *output, size_t output_len);
+/* Same on device-resident buffers, enqueued on `hip_stream` (NULL = the
+ * handle's own stream), asynchronous: channel c reads d_input[c*in_stride ..
+ * + len] and writes d_output[c*out_stride .. + len]. */
+int fftconv_uniform_process_device(fftconv_uniform *h, const float *d_input, size_t in_stride,
+                                   float *d_output, size_t out_stride, size_t len, void *hip_stream);
+/* #[derive(Clone)]: a deep, device-side copy of every buffer and scalar. */
+fftconv_uniform *fftconv_uniform_clone(const fftconv_uniform *h);
+void fftconv_uniform_destroy(fftconv_uniform *h);
+int fftconv_uniform_synchronize(fftconv_uniform *h);
+size_t fftconv_uniform_channels(const fftconv_uniform *h);
+size_t fftconv_uniform_block_size(const fftconv_uniform *h);   /* next_power_of_two(max_block_size) */
+size_t fftconv_uniform_seg_count(const fftconv_uniform *h);
+/* copies {current, active_seg_count, input_buffer_fill} of one channel */
+int fftconv_uniform_channel_state(const fftconv_uniform *h, size_t channel, size_t out3[3]);
+
+/* ---- TwoStageFFTConvolver (head block + García-optimal tail block) ----- */
+fftconv_twostage *fftconv_twostage_init(const float *response, size_t response_len,
+                                        size_t max_block_size, size_t max_response_length);
+fftconv_twostage *fftconv_twostage_init_batch(int device, size_t channels, const float *responses,
+                                              size_t response_len, size_t response_stride,
+                                              size_t max_block_size, size_t max_response_length);
+/* todo!() in the reference (src/fft_convolver.rs:422-424): FFTCONV_E_UNIMPLEMENTED. */
+int fftconv_twostage_update(fftconv_twostage *h, const float *response, size_t response_len);
+int fftconv_twostage_reset(fftconv_twostage *h);
+/* len must be <= max_block_size (assert at src/fft_convolver.rs:428); input and
+ * output both [channels][len]. */
+int fftconv_twostage_process(fftconv_twostage *h, const float *input, float *output, size_t len);
+int fftconv_twostage_process_device(fftconv_twostage *h, const float *d_input, size_t in_stride,
+                                    float *d_output, size_t out_stride, size_t len, void *hip_stream);
+fftconv_twostage *fftconv_twostage_clone(const fftconv_twostage *h);
+void fftconv_twostage_destroy(fftconv_twostage *h);
+int fftconv_twostage_synchronize(fftconv_twostage *h);
+size_t fftconv_twostage_tail_block_size(const fftconv_twostage *h);
+
+/* ---- CrossfadeConvolver<FFTConvolver> ---------------------------------- */
+/* Convolution::init, src/crossfade_convolver.rs:46-49: crossfade_samples =
+ * response_len, hold = min(max_block_size, response_len). */
+fftconv_crossfade *fftconv_crossfade_init(const float *response, size_t response_len,
+                                          size_t max_block_size, size_t max_response_length);
+fftconv_crossfade *fftconv_crossfade_init_batch(int device, size_t channels, const float *responses,
+                                                size_t response_len, size_t response_stride,
+                                                size_t max_block_size, size_t max_response_length);
+/* CrossfadeConvolver::new, src/crossfade_convolver.rs:19-43.  `convolver` is
+ * cloned (the reference moves it; the caller keeps ownership of its handle). */
+fftconv_crossfade *fftconv_crossfade_new(const fftconv_uniform *convolver, size_t max_response_length,
+                                         size_t max_buffer_size, size_t crossfade_samples);
+/* src/crossfade_convolver.rs:51-64; same response for every channel. */
+int fftconv_crossfade_update(fftconv_crossfade *h, const float *response, size_t response_len);
+int fftconv_crossfade_update_batch(fftconv_crossfade *h, const float *responses, size_t response_len,
+                                   size_t response_stride);
+/* todo!() in the reference (src/crossfade_convolver.rs:80-82): FFTCONV_E_UNIMPLEMENTED. */
+int fftconv_crossfade_reset(fftconv_crossfade *h);
+/* src/crossfade_convolver.rs:66-78: input_len >= max_buffer_size and
+ * output_len <= max_buffer_size (the reference's slice bounds). */
+int fftconv_crossfade_process(fftconv_crossfade *h, const float *input, size_t input_len,
+                              float *output, size_t output_len);
+int fftconv_crossfade_process_device(fftconv_crossfade *h, const float *d_input, size_t in_stride,
+                                     float *d_output, size_t out_stride, size_t output_len,
+                                     void *hip_stream);
+int fftconv_crossfade_is_crossfading(const fftconv_crossfade *h); /* :85-92, 1/0 */
+fftconv_crossfade *fftconv_crossfade_clone(const fftconv_crossfade *h);
+void fftconv_crossfade_destroy(fftconv_crossfade *h);
+int fftconv_crossfade_synchronize(fftconv_crossfade *h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FFTCONV_H */

@@ -1,0 +1,435 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the f64
+ground truth, plus the reference's own tests (src/tests.rs, inline #[test]s)
+re-run on the device.  Tolerance: max|gpu - ref| <= 1e-5 * max|ref|
+(REL_TOL), 1e-6 absolute for the delta-IR known answers (as the reference)."""
+import numpy as np
+import pytest
+
+from common import DELTA_ABS_TOL, REL_TOL, assert_close, generate_sinusoid, ir, white
+
+pytestmark = pytest.mark.gpu
+
+
+def run_chunks(conv, x, chunks):
+    ys, p = [], 0
+    for k in chunks:
+        ys.append(conv.process(x[..., p:p + k]))
+        p += k
+    return np.concatenate(ys, axis=-1)
+
+
+# ---------------------------------------------------------------------------
+# the reference's inline tests, on the device
+# ---------------------------------------------------------------------------
+def test_fft_convolver_passthrough(amd):
+    """src/fft_convolver.rs:323-335."""
+    response = np.zeros(1024, np.float32)
+    response[0] = 1.0
+    conv = amd.FFTConvolver.init(response, 1024, response.size)
+    out = conv.process(np.ones(1024, np.float32))
+    assert np.max(np.abs(out - 1.0)) < DELTA_ABS_TOL
+
+
+def test_fft_twostage_convolver_passthrough(amd):
+    """src/fft_convolver.rs:542-554."""
+    response = np.zeros(1024, np.float32)
+    response[0] = 1.0
+    conv = amd.TwoStageFFTConvolver.init(response, 1024, response.size)
+    out = conv.process(np.ones(1024, np.float32))
+    assert np.max(np.abs(out - 1.0)) < DELTA_ABS_TOL
+
+
+def test_crossfade_convolver_passthrough(amd):
+    """src/crossfade_convolver.rs:107-124."""
+    response = np.zeros(1024, np.float32)
+    response[0] = 1.0
+    conv = amd.CrossfadeConvolver.new(amd.FFTConvolver.init(response, 1024, response.size), 1024, 1024, 1024)
+    out = conv.process(np.ones(1024, np.float32))
+    assert np.max(np.abs(out - 1.0)) < DELTA_ABS_TOL
+
+
+# ---------------------------------------------------------------------------
+# src/tests.rs, on the device
+# ---------------------------------------------------------------------------
+def test_fft_convolver_update_is_reset(amd):
+    """src/tests.rs:18-59."""
+    bs = 512
+    ra = generate_sinusoid(bs, 1000.0, gain=1.0)
+    rb = generate_sinusoid(bs, 2000.0, gain=0.7)
+    ca = amd.FFTConvolver.init(ra, bs, ra.size)
+    cb = amd.FFTConvolver.init(rb, bs, rb.size)
+    cu = amd.FFTConvolver.init(ra, bs, ra.size)
+    x = generate_sinusoid(16 * bs, 1300.0)
+    for i in range(16):
+        blk = x[i * bs:(i + 1) * bs]
+        if i == 8:
+            cu.update(rb)
+        ou = cu.process(blk)
+        ref = ca.process(blk) if i < 8 else cb.process(blk)
+        assert np.max(np.abs(ref - ou)) < 1e-6, i
+
+
+def test_crossfade_convolver(amd):
+    """src/tests.rs:61-117."""
+    bs = 512
+    ra = generate_sinusoid(bs, 1000.0, gain=1.0)
+    rb = generate_sinusoid(bs, 2000.0, gain=0.7)
+    ca = amd.FFTConvolver.init(ra, bs, ra.size)
+    cb = amd.FFTConvolver.init(rb, bs, rb.size)
+    xf = amd.CrossfadeConvolver.new(ca.clone(), bs, bs, bs)
+    x = generate_sinusoid(16 * bs, 1300.0)
+    for i in range(16):
+        blk = x[i * bs:(i + 1) * bs]
+        if i == 8:
+            xf.update(rb)
+        oc = xf.process(blk)
+        oa = ca.process(blk)
+        if i >= 8:
+            ob = cb.process(blk)
+        if i <= 8:
+            assert np.max(np.abs(oa - oc)) < 1e-6, i
+        elif i == 9:
+            j = bs // 2 - 1
+            assert abs(oc[j] - (oa[j] * 0.5 + ob[j] * 0.5)) < 1e-6
+        else:
+            assert np.max(np.abs(ob - oc)) < 1e-6, i
+
+
+def test_block_size_equal(amd):
+    """src/tests.rs:119-146 (multi-block-per-call path)."""
+    bs = 128
+    response = generate_sinusoid(bs, 1000.0, gain=0.1)
+    ca = amd.FFTConvolver.init(response, bs // 2, response.size)
+    cb = amd.FFTConvolver.init(response, bs, response.size)
+    x = generate_sinusoid(1000 * bs, 1300.0, gain=0.1)
+    for i in range(1000):
+        blk = x[i * bs:(i + 1) * bs]
+        assert np.max(np.abs(ca.process(blk) - cb.process(blk))) < 1e-5, i
+
+
+def test_twostage_equal(amd):
+    """src/tests.rs:148-175."""
+    bs = 64
+    response = generate_sinusoid(12000, 1000.0, gain=0.1)
+    ca = amd.FFTConvolver.init(response, bs // 2, response.size)
+    cb = amd.TwoStageFFTConvolver.init(response, bs, response.size)
+    assert cb.tail_block_size == 1024
+    x = generate_sinusoid(1000 * bs, 1300.0, gain=0.1)
+    for i in range(1000):
+        blk = x[i * bs:(i + 1) * bs]
+        assert np.max(np.abs(ca.process(blk) - cb.process(blk))) < 1e-5, i
+
+
+@pytest.mark.parametrize("kind", ["uniform", "twostage"])
+def test_reset(amd, kind):
+    """src/tests.rs:177-257."""
+    bs, n = 64, 1000
+    response = generate_sinusoid(12000, 1000.0, gain=0.1)
+    cls = amd.FFTConvolver if kind == "uniform" else amd.TwoStageFFTConvolver
+    conv = cls.init(response, bs, response.size)
+    x = generate_sinusoid(n * bs, 1300.0, gain=0.1)
+    a = np.concatenate([conv.process(x[i * bs:(i + 1) * bs]) for i in range(n)])
+    conv.reset()
+    b = np.concatenate([conv.process(x[i * bs:(i + 1) * bs]) for i in range(n)])
+    assert np.max(np.abs(a - b)) < 1e-5
+
+
+# ---------------------------------------------------------------------------
+# parity with the oracle restatement (same inputs)
+# ---------------------------------------------------------------------------
+UNIFORM_CASES = [
+    # (block, ir_len, chunk pattern)  -- pattern repeats to cover > S blocks
+    (256, 4096, [256]),                 # cfg1 geometry
+    (64, 12000, [64]),
+    (1, 7, [1, 3, 2]),                  # B = 1 (N = 2)
+    (2, 9, [1, 2, 5]),
+    (4, 33, [4, 3, 9]),
+    (8, 100, [8]),
+    (32, 500, [32, 7, 100]),
+    (100, 1000, [128, 17, 300]),        # block 100 -> 128
+    (512, 1000, [100, 300, 1000, 17, 512]),
+    (1024, 5000, [1024, 2048, 5]),
+    (2048, 9000, [2048]),
+    (4096, 20000, [4096, 1000]),
+    (8192, 20000, [8192]),
+]
+
+
+@pytest.mark.parametrize("block,L,pattern", UNIFORM_CASES)
+def test_uniform_vs_oracle(amd, oracle_mod, block, L, pattern):
+    rng = np.random.default_rng(block * 7 + L)
+    h = ir(rng, L)
+    conv = amd.FFTConvolver.init(h, block, L)
+    ref = oracle_mod.FFTConvolver.init(h, block, L)
+    S = ref.seg_count
+    chunks, tot = [], 0
+    while tot < (S + 3) * ref.block_size or len(chunks) < 8:
+        for k in pattern:
+            chunks.append(k)
+            tot += k
+    x = white(rng, tot)
+    got = run_chunks(conv, x, chunks)
+    exp = run_chunks(ref, x, chunks)
+    assert_close(got, exp, what=f"B={block} L={L}")
+    assert_close(got, oracle_mod.direct_convolution(x, h), what="vs f64")
+    assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
+
+
+def test_uniform_batch_distinct_channels(amd, oracle_mod):
+    rng = np.random.default_rng(5)
+    C, B, L = 8, 256, 3000
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    x = np.stack([white(rng, 40 * B) for _ in range(C)])
+    chunks = [B] * 30 + [100, 156, 3 * B, 256, 5 * B]
+    got = run_chunks(conv, x, chunks)
+    for c in range(C):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        assert_close(got[c], run_chunks(ref, x[c], chunks), what=f"channel {c}")
+
+
+def test_uniform_update_sequence(amd, oracle_mod):
+    """update() keeps the FDL/current/fill and zeroes overlap+pre (:188-227),
+    including a mid-block update and a shrinking active_seg_count."""
+    rng = np.random.default_rng(11)
+    B, L = 64, 1000
+    h0 = ir(rng, L)
+    conv = amd.FFTConvolver.init(h0, B, L)
+    ref = oracle_mod.FFTConvolver.init(h0, B, L)
+    script = [("p", 64)] * 20 + [("u", 1000), ("p", 64), ("p", 30), ("u", 130), ("p", 50), ("p", 64)] \
+        + [("p", 64)] * 5 + [("u", 0), ("p", 64), ("u", 700)] + [("p", 64)] * 25 + [("p", 7), ("u", 64), ("p", 200)]
+    for op, n in script:
+        if op == "p":
+            x = white(rng, n)
+            assert_close(conv.process(x), ref.process(x), what=f"{op}{n}")
+        else:
+            hn = ir(rng, n)
+            conv.update(hn)
+            ref.update(hn)
+        assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
+
+
+def test_uniform_update_channel(amd, oracle_mod):
+    rng = np.random.default_rng(12)
+    C, B, L = 4, 128, 900
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    refs = [oracle_mod.FFTConvolver.init(hs[c], B, L) for c in range(C)]
+    for step in range(30):
+        if step == 10:
+            hn = ir(rng, 300)
+            conv.update_channel(2, hn)
+            refs[2].update(hn)
+        x = np.stack([white(rng, B) for _ in range(C)])
+        got = conv.process(x)
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"step {step} ch {c}")
+
+
+def test_uniform_clone(amd, oracle_mod):
+    rng = np.random.default_rng(13)
+    B, L = 256, 2000
+    h = ir(rng, L)
+    conv = amd.FFTConvolver.init(h, B, L)
+    ref = oracle_mod.FFTConvolver.init(h, B, L)
+    for _ in range(5):
+        x = white(rng, 300)
+        conv.process(x)
+        ref.process(x)
+    twin = conv.clone()
+    rtwin = ref.clone()
+    for _ in range(12):
+        x = white(rng, B)
+        a, b = conv.process(x), twin.process(x)
+        assert np.array_equal(a, b)
+        assert_close(a, ref.process(x))
+        rtwin.process(x)
+
+
+def test_uniform_nonfinite_zero_fills(amd, oracle_mod):
+    """A NaN makes realfft's C2R fail; the reference zero-fills the output and
+    leaves fill/current where they were (src/fft_convolver.rs:278-281)."""
+    rng = np.random.default_rng(14)
+    B, L = 64, 500
+    h = ir(rng, L)
+    conv = amd.FFTConvolver.init(h, B, L)
+    ref = oracle_mod.FFTConvolver.init(h, B, L)
+    seq = []
+    for i in range(20):
+        x = white(rng, B if i % 3 else 40)
+        if i in (6, 13):
+            x[5] = np.nan
+        seq.append(x)
+    for x in seq:
+        g, r = conv.process(x), ref.process(x)
+        assert np.array_equal(np.isnan(g), np.isnan(r))
+        m = ~np.isnan(r)
+        assert_close(g[m], r[m])
+        assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
+
+
+def test_uniform_edge_geometries(amd, oracle_mod):
+    # empty IR / zero max length: Default-like convolver outputs zeros
+    conv = amd.FFTConvolver.init(np.zeros(0, np.float32), 64, 0)
+    assert np.all(conv.process(np.ones(100, np.float32)) == 0)
+    conv.update(np.zeros(0, np.float32))  # ir_len == 0: early return
+    # update with an empty response: active_seg_count = 0 -> zeros
+    h = ir(np.random.default_rng(1), 300)
+    conv = amd.FFTConvolver.init(h, 64, 300)
+    conv.process(np.ones(64, np.float32))
+    conv.update(np.zeros(0, np.float32))
+    assert np.all(conv.process(np.ones(64, np.float32)) == 0)
+    # zero-length process
+    assert conv.process(np.ones(0, np.float32)).size == 0
+
+
+def test_uniform_panics(amd):
+    with pytest.raises(amd.ConvolutionPanic):
+        amd.FFTConvolver.init(np.ones(10, np.float32), 4, 5)
+    conv = amd.FFTConvolver.init(np.ones(10, np.float32), 4, 10)
+    with pytest.raises(amd.ConvolutionPanic):
+        conv.update(np.ones(11, np.float32))
+    with pytest.raises(amd.ConvolutionPanic):
+        conv.process(np.ones(4, np.float32), out_len=8)
+    with pytest.raises(amd.DeviceError):
+        amd.FFTConvolver.init(np.ones(10, np.float32), 16384, 10)
+
+
+@pytest.mark.parametrize("head,L,calls", [(64, 12000, [64]), (32, 5000, [32, 13, 19]), (32, 3000, [1, 31, 32, 16]),
+                                          (128, 200, [128]), (64, 262144, [64])])
+def test_twostage_vs_oracle(amd, oracle_mod, head, L, calls):
+    rng = np.random.default_rng(head + L)
+    h = ir(rng, L)
+    conv = amd.TwoStageFFTConvolver.init(h, head, L)
+    ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
+    assert conv.tail_block_size == ref.tail_block_size
+    T = ref.tail_block_size
+    n_calls = max(3 * T // max(min(calls), 1), 40)
+    if L >= 200000:
+        n_calls = 2 * T // head + 5  # past both tail swaps
+    chunks = [calls[i % len(calls)] for i in range(n_calls)]
+    x = white(rng, sum(chunks))
+    got = run_chunks(conv, x, chunks)
+    exp = run_chunks(ref, x, chunks)
+    assert_close(got, exp, what=f"two-stage {head}/{L}")
+    assert_close(got, oracle_mod.direct_convolution(x, h), what="vs f64")
+
+
+def test_twostage_non_power_of_two_head_panics(amd):
+    conv = amd.TwoStageFFTConvolver.init(np.ones(5000, np.float32), 48, 5000)
+    assert conv.tail_block_size == 512
+    for _ in range(10):
+        conv.process(np.ones(48, np.float32))
+    with pytest.raises(amd.ConvolutionPanic):
+        conv.process(np.ones(48, np.float32))
+
+
+def test_twostage_panics(amd):
+    conv = amd.TwoStageFFTConvolver.init(np.ones(100, np.float32), 32, 100)
+    with pytest.raises(amd.ConvolutionPanic):
+        conv.process(np.ones(33, np.float32))
+    with pytest.raises(amd.NotImplementedInReference):
+        conv.update(np.ones(10, np.float32))
+
+
+def test_twostage_clone(amd):
+    rng = np.random.default_rng(21)
+    h = ir(rng, 5000)
+    conv = amd.TwoStageFFTConvolver.init(h, 32, 5000)
+    for _ in range(50):
+        conv.process(white(rng, 32))
+    twin = conv.clone()
+    for _ in range(80):
+        x = white(rng, 32)
+        assert np.array_equal(conv.process(x), twin.process(x))
+
+
+@pytest.mark.parametrize("B,L,every,xfade", [(512, 2000, 5, None), (64, 700, 3, None), (128, 1000, 7, 300),
+                                             (256, 256, 2, None)])
+def test_crossfade_vs_oracle(amd, oracle_mod, B, L, every, xfade):
+    """update every `every` blocks: exercises fade, hold, and the pending path
+    (the trait init fades over response.len() samples, src/crossfade_convolver.rs:46-49)."""
+    rng = np.random.default_rng(B + L + every)
+    h = ir(rng, L)
+    if xfade is None:
+        conv = amd.CrossfadeConvolver.init(h, B, L)
+        ref = oracle_mod.CrossfadeConvolver.init(h, B, L)
+    else:
+        conv = amd.CrossfadeConvolver.new(amd.FFTConvolver.init(h, B, L), L, B, xfade)
+        ref = oracle_mod.CrossfadeConvolver.new(oracle_mod.FFTConvolver.init(h, B, L), L, B, xfade)
+    for i in range(40):
+        if i % every == every - 1:
+            hn = ir(rng, int(rng.integers(1, L + 1)))
+            conv.update(hn)
+            ref.update(hn)
+        x = white(rng, B)
+        out_len = B if i % 4 else B // 2
+        assert_close(conv.process(x, out_len), ref.process(x, out_len), what=f"block {i}")
+        assert conv.is_crossfading() == ref.is_crossfading()
+
+
+def test_crossfade_batch(amd, oracle_mod):
+    rng = np.random.default_rng(31)
+    C, B, L = 3, 128, 600
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.CrossfadeConvolver.init(hs, B, L, channels=C)
+    refs = [oracle_mod.CrossfadeConvolver.init(hs[c], B, L) for c in range(C)]
+    for i in range(25):
+        if i in (4, 9, 15):
+            hn = np.stack([ir(rng, 400) for _ in range(C)])
+            conv.update(hn)
+            for c in range(C):
+                refs[c].update(hn[c])
+        x = np.stack([white(rng, B) for _ in range(C)])
+        got = conv.process(x)
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"block {i} ch {c}")
+
+
+def test_crossfade_panics(amd):
+    conv = amd.CrossfadeConvolver.init(np.ones(100, np.float32), 32, 100)
+    with pytest.raises(amd.NotImplementedInReference):
+        conv.reset()
+    with pytest.raises(amd.ConvolutionPanic):
+        conv.process(np.ones(16, np.float32))          # input shorter than max_buffer_size
+    with pytest.raises(amd.ConvolutionPanic):
+        conv.process(np.ones(64, np.float32), out_len=33)
+
+
+# ---------------------------------------------------------------------------
+# the north-star geometry (cfg2) at full size
+# ---------------------------------------------------------------------------
+def test_cfg2_full_size_sampled_channels(amd, oracle_mod):
+    """1024 channels x IR 48000, block 256, device-resident path.  Sampled
+    channels against the oracle over > S blocks (the FDL ring wraps), and
+    linearity of the whole batch."""
+    import torch
+
+    C, B, L, steps = 1024, 256, 48000, 200
+    rng = np.random.default_rng(2024)
+    hs = (rng.uniform(-1, 1, (C, L)) / np.sqrt(L)).astype(np.float32)
+    x = rng.uniform(-1, 1, (C, steps * B)).astype(np.float32)
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    dev = torch.device("cuda:0")
+    xd = torch.from_numpy(x).to(dev)
+    yd = torch.empty_like(xd)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(s)
+    stream = s.cuda_stream
+    assert stream != 0
+    for s in range(steps):
+        conv.process_device(xd.data_ptr() + 4 * s * B, steps * B, yd.data_ptr() + 4 * s * B, steps * B, B, stream)
+    torch.cuda.synchronize()
+    y = yd.cpu().numpy()
+    for c in (0, 1, 511, 1023):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        exp = np.concatenate([ref.process(x[c, s * B:(s + 1) * B]) for s in range(steps)])
+        assert_close(y[c], exp, what=f"channel {c}")
+    # linearity on every channel: conv(2x) == 2 conv(x) exactly in binary f32 scaling
+    conv2 = amd.FFTConvolver.init(hs, B, L, channels=C)
+    y2d = torch.empty_like(xd)
+    x2d = xd * 2.0
+    for s in range(steps):
+        conv2.process_device(x2d.data_ptr() + 4 * s * B, steps * B, y2d.data_ptr() + 4 * s * B, steps * B, B, stream)
+    torch.cuda.synchronize()
+    assert torch.equal(y2d, 2.0 * yd)
