@@ -754,6 +754,13 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
     return next_pow2(bi);
 }
 
+int fftconv_set_kernel_variant(int variant) {
+    if (variant >= 0 && (variant & 0xff) > 3) return fail(FFTCONV_E_INVALID, "variant bits must be 0..3 (or -1 = auto)");
+    set_variant(variant);
+    return FFTCONV_OK;
+}
+int fftconv_get_kernel_variant(void) { return get_variant(); }
+
 // ---- uniform --------------------------------------------------------------
 fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len, size_t max_block_size,
                                       size_t max_response_length) {

@@ -72,6 +72,28 @@ template <int VEC> using AccT = std::conditional_t<VEC == 2, Acc2, Acc1>;
 __device__ __forceinline__ float4 vadd(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 __device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 
+// 16-/8-byte loads of the H / X streams; NTL = nontemporal (streamed once per step)
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <bool NTL>
+__device__ __forceinline__ float4 ldv(const float4 *p) {
+    if constexpr (NTL) {
+        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+template <bool NTL>
+__device__ __forceinline__ float2 ldv(const float2 *p) {
+    if constexpr (NTL) {
+        const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v *>(p));
+        return make_float2(v.x, v.y);
+    } else {
+        return *p;
+    }
+}
+
 // conv = pre + x (.) h for one slot, packed-aware (slot 0 bin 0 is (DC, Nyquist)).
 __device__ __forceinline__ float4 slot_mac(float4 pre, float4 x, float4 h, int slot) {
     float4 r;
@@ -92,14 +114,66 @@ __device__ __forceinline__ float2 slot_mac(float2 pre, float2 x, float2 h, int) 
 __device__ __forceinline__ bool slot0_finite(float4 v) { return isfinite(v.x) && isfinite(v.y); }
 __device__ __forceinline__ bool slot0_finite(float2 v) { return isfinite(v.x) && isfinite(v.y); }
 
+// pre_multiplied = sum_{i=1}^{act-1} H[i] (.) X[(cur+i) % act] over this
+// thread's slots (src/fft_convolver.rs:258-269).  Rows i = 1..act-1 are
+// visited in scan order t = 0..act-2, group g taking t = g (mod G).
+// ZZ: every other block scans the rows backwards (rows read last by one step
+// are read first by the next).  NTL: nontemporal loads.
+template <int LOG2B, int NT, bool ZZ, bool NTL, class AccArr>
+__device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const float2 *Xc, int cur, int act,
+                                         int flags, int f0, int g) {
+    using Gm = Geo<LOG2B, NT>;
+    constexpr int B = Gm::B, VEC = Gm::VEC, G = Gm::G, SPT = Gm::SPT, U = Gm::U;
+    using vec_t = typename VecT<VEC>::type;
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) acc[s].zero();
+    const bool rev = ZZ && (flags & FLAG_REV);
+    const int di = rev ? -G : G;
+    int t = g;
+    int i = rev ? act - 1 - t : 1 + t;
+    int xi = (cur + i) % act;  // index_audio = (current + i) % active
+    for (; t + (U - 1) * G < act - 1; t += U * G) {
+        vec_t hv[U][SPT], xv[U][SPT];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)i * B);
+            const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xi * B);
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+                hv[u][s] = ldv<NTL>(hrow + f0 + s * NT);
+                xv[u][s] = ldv<NTL>(xrow + f0 + s * NT);
+            }
+            i += di;
+            xi += di;
+            if (xi >= act) xi -= act;
+            if (xi < 0) xi += act;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) acc[s].mac(hv[u][s], xv[u][s]);
+    }
+    for (; t < act - 1; t += G) {
+        const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)i * B);
+        const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xi * B);
+#pragma unroll
+        for (int s = 0; s < SPT; ++s)
+            acc[s].mac(ldv<NTL>(hrow + f0 + s * NT), ldv<NTL>(xrow + f0 + s * NT));
+        i += di;
+        xi += di;
+        if (xi >= act) xi -= act;
+        if (xi < 0) xi += act;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Fused UPOLS step: FFTConvolver::process (src/fft_convolver.rs:229-309) for
 // one channel per workgroup, the whole chunk loop of one call on device.
 // ---------------------------------------------------------------------------
-template <int LOG2B, int NT>
+template <int LOG2B, int NT, bool ZZ, bool NTL>
 __global__ __launch_bounds__(NT) void upols_process_kernel(ProcArgs a) {
     using Gm = Geo<LOG2B, NT>;
-    constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT, U = Gm::U;
+    constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT;
     constexpr float invN = 1.0f / (float)(2 * B);
     using vec_t = typename VecT<VEC>::type;
 
@@ -153,41 +227,12 @@ __global__ __launch_bounds__(NT) void upols_process_kernel(ProcArgs a) {
 
         if (was_empty) {                                                 // :258-269
             AccT<VEC> acc[SPT];
-#pragma unroll
-            for (int s = 0; s < SPT; ++s) acc[s].zero();
-            int i = 1 + g;
-            int xi = act > 0 ? (cur + i) % act : 0;  // index_audio = (current + i) % active
-            for (; i + (U - 1) * G < act; i += U * G) {
-                vec_t hv[U][SPT], xv[U][SPT];
-                int xr = xi;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)(i + u * G) * B);
-                    const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xr * B);
-#pragma unroll
-                    for (int s = 0; s < SPT; ++s) {
-                        hv[u][s] = hrow[f0 + s * NT];
-                        xv[u][s] = xrow[f0 + s * NT];
-                    }
-                    xr += G;
-                    if (xr >= act) xr -= act;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int s = 0; s < SPT; ++s) acc[s].mac(hv[u][s], xv[u][s]);
-                xi = xr;
-            }
-            for (; i < act; i += G) {
-                const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)i * B);
-                const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xi * B);
-#pragma unroll
-                for (int s = 0; s < SPT; ++s)
-                    acc[s].mac(hrow[f0 + s * NT],
-                               xrow[f0 + s * NT]);
-                xi += G;
-                if (xi >= act) xi -= act;
-            }
+            // hot channels (index < a.hot) stream with plain loads so they can
+            // stay resident in the Infinity Cache; the rest stream nontemporally
+            if (NTL && (int)c >= a.hot)
+                mac_rows<LOG2B, NT, ZZ, true>(acc, Hc, Xc, cur, act, flags, f0, g);
+            else
+                mac_rows<LOG2B, NT, ZZ, false>(acc, Hc, Xc, cur, act, flags, f0, g);
             if constexpr (G > 1) {
                 red[g * F + f0] = acc[0].get(f0);
                 __syncthreads();
@@ -263,6 +308,7 @@ __global__ __launch_bounds__(NT) void upols_process_kernel(ProcArgs a) {
             if (flags & FLAG_INBUF)
                 for (int j = tid; j < B; j += NT) ibc[j] = 0.f;           // :294
             flags &= ~FLAG_INBUF;
+            flags ^= FLAG_REV;
             fill = 0;
             cur = cur > 0 ? cur - 1 : act - 1;                            // :301-305
         } else {
@@ -407,16 +453,38 @@ __global__ void reset_state_kernel(int4 *state, int channels) {
 // ---------------------------------------------------------------------------
 constexpr int kNT = 256;
 
+static int g_variant = VARIANT_AUTO;
+static int g_hot = 0;
+
+// Automatic variant: a per-step H+X stream larger than the 256 MiB Infinity
+// Cache is re-read from HBM every step whatever the load policy, and there
+// nontemporal loads stream 12-14 % faster (measured, cfg2: 137 -> 121 us);
+// a stream that stays cache-resident across steps is 1.5x faster with plain
+// loads (S = 8: 9.5 vs 14.3 us).  Zig-zag adds ~0.6 % on top of NT only.
+static int pick_variant(const ProcArgs &a, int channels, int log2b) {
+    if (g_variant != VARIANT_AUTO) return g_variant;
+    const double stream = 16.0 * (double)channels * (double)a.S * (double)(1 << log2b);
+    return stream > 192.0 * 1024 * 1024 ? (VARIANT_NT | VARIANT_ZIGZAG) : 0;
+}
+
 template <int LOG2B>
 static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t s) {
     using Gm = Geo<LOG2B, kNT>;
-    auto kern = upols_process_kernel<LOG2B, kNT>;
+    auto kern = upols_process_kernel<LOG2B, kNT, false, false>;
+    switch (pick_variant(a, channels, LOG2B) & 3) {
+        case 1: kern = upols_process_kernel<LOG2B, kNT, true, false>; break;
+        case 2: kern = upols_process_kernel<LOG2B, kNT, false, true>; break;
+        case 3: kern = upols_process_kernel<LOG2B, kNT, true, true>; break;
+        default: break;
+    }
     if (Gm::lds_bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)Gm::lds_bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(channels), dim3(kNT), Gm::lds_bytes, s, a);
+    ProcArgs b = a;
+    b.hot = g_hot;
+    hipLaunchKernelGGL(kern, dim3(channels), dim3(kNT), Gm::lds_bytes, s, b);
     return hipGetLastError();
 }
 
@@ -472,6 +540,12 @@ hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStre
     hipLaunchKernelGGL(crossfade_mix_kernel, dim3(channels), dim3(256), 0, s, a);
     return hipGetLastError();
 }
+
+void set_variant(int v) {
+    g_variant = v < 0 ? VARIANT_AUTO : (v & 0xff);
+    g_hot = v < 0 ? 0 : v >> 8;
+}
+int get_variant() { return g_variant == VARIANT_AUTO ? -1 : (g_variant | (g_hot << 8)); }
 
 hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;

@@ -5,7 +5,15 @@
 
 namespace fftconv {
 
-enum : int { FLAG_INBUF = 1 };  // the HBM input buffer holds live samples
+enum : int {
+    FLAG_INBUF = 1,  // the HBM input buffer holds live samples
+    FLAG_REV = 2,    // scan parity of the segment MAC (toggled per completed block)
+};
+
+// fused-kernel variants (bit mask): 1 = zig-zag segment scan, 2 = nontemporal H/X loads
+enum : int { VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_AUTO = 0x7fffffff };
+void set_variant(int v);
+int get_variant();
 
 struct ProcArgs {
     const float2 *H;       // [C][S][B] packed IR spectra
@@ -21,6 +29,7 @@ struct ProcArgs {
     const float2 *tw;      // W_N^k, k < N = 2B
     int S;                 // seg_count (row pitch of H and X in rows)
     int n;                 // output samples this call
+    int hot;               // channels [0, hot) use cache-allocating loads (NT variants)
 };
 
 struct IrArgs {

@@ -41,6 +41,8 @@ SIGNATURES = {
     "fftconv_device_count": (_i, []),
     "fftconv_complex_size": (_sz, [_sz]),
     "fftconv_compute_tail_block_size": (_sz, [_sz, _sz]),
+    "fftconv_set_kernel_variant": (_i, [_i]),
+    "fftconv_get_kernel_variant": (_i, []),
     "fftconv_uniform_init": (_vp, [_fp, _sz, _sz, _sz]),
     "fftconv_uniform_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
     "fftconv_uniform_update": (_i, [_vp, _fp, _sz]),
@@ -161,6 +163,14 @@ def complex_size(n: int) -> int:
 
 def compute_tail_block_size(head_len: int, response_len: int) -> int:
     return int(lib().fftconv_compute_tail_block_size(head_len, response_len))
+
+
+def set_kernel_variant(v: int):
+    _check(lib().fftconv_set_kernel_variant(v))
+
+
+def get_kernel_variant() -> int:
+    return int(lib().fftconv_get_kernel_variant())
 
 
 def device_count() -> int:

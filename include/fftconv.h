@@ -58,6 +58,13 @@ const char *fftconv_last_error(void);            /* thread-local, "" if none */
 int fftconv_device_count(void);                   /* visible HIP devices, 0 if none */
 size_t fftconv_complex_size(size_t size);         /* src/fft_convolver.rs:66-68 */
 size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /* :534-540 */
+/* Tuning knob (process-wide): spectral-MAC scan variant of the fused kernel,
+ * -1 = automatic (default: nontemporal + zig-zag when the per-step H+X
+ * stream exceeds the Infinity Cache, plain loads otherwise), else bit 0 =
+ * zig-zag segment order on alternate blocks, bit 1 = nontemporal H/X loads.
+ * Results agree within f32 rounding across variants. */
+int fftconv_set_kernel_variant(int variant);
+int fftconv_get_kernel_variant(void);
 
 /* ---- FFTConvolver (uniformly partitioned, zero latency) ---------------- */
 /* FFTConvolver::init, src/fft_convolver.rs:119-186.  NULL on error. */

@@ -175,6 +175,32 @@ def test_uniform_vs_oracle(amd, oracle_mod, block, L, pattern):
     assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_uniform_kernel_variants(amd, oracle_mod, variant):
+    """Every fused-kernel variant (zig-zag scan / nontemporal loads) against the
+    oracle, with partial chunks, multi-block calls and an update in between."""
+    rng = np.random.default_rng(40 + variant)
+    C, B, L = 3, 256, 5000
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    amd.set_kernel_variant(variant)
+    try:
+        conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+        refs = [oracle_mod.FFTConvolver.init(hs[c], B, L) for c in range(C)]
+        chunks = [B] * 25 + [100, 156, 3 * B, 7] + [B] * 5
+        for j, k in enumerate(chunks):
+            if j == 27:
+                hn = np.stack([ir(rng, 3000) for _ in range(C)])
+                conv.update(hn)
+                for c in range(C):
+                    refs[c].update(hn[c])
+            x = np.stack([white(rng, k) for _ in range(C)])
+            got = conv.process(x)
+            for c in range(C):
+                assert_close(got[c], refs[c].process(x[c]), what=f"variant {variant} chunk {j} ch {c}")
+    finally:
+        amd.set_kernel_variant(-1)
+
+
 def test_uniform_batch_distinct_channels(amd, oracle_mod):
     rng = np.random.default_rng(5)
     C, B, L = 8, 256, 3000
