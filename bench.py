@@ -56,18 +56,60 @@ def parse():
     p.add_argument("--ring", type=int, default=32, help="distinct input/output blocks kept in HBM")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU time per baseline leg")
-    p.add_argument("--traffic", default="", help="JSON file with PMC traffic (profiles/*pmc*.json) to attach")
+    p.add_argument("--pmc", choices=["auto", "off"], default="auto",
+                   help="collect HBM traffic with two rocprofv3 --pmc child passes (N=1, rank 0)")
+    p.add_argument("--pmc-inner", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
 
-def make_irs(rank: int, C: int, L: int) -> np.ndarray:
-    """Distinct IR per global channel: U[-1,1)/sqrt(L), seed 1234 + channel."""
-    out = np.empty((C, L), np.float32)
-    scale = 1.0 / np.sqrt(L)
-    for c in range(C):
-        g = np.random.default_rng(1234 + rank * C + c)
-        out[c] = g.uniform(-1.0, 1.0, L) * scale
-    return out
+def pmc_traffic(args):
+    """HBM bytes per launch of the fused kernel from two separate rocprofv3
+    --pmc passes of this same workload (FETCH_SIZE, then WRITE_SIZE), corrected
+    as MI355X_MICROARCH.md §HBM prescribes: read = 2 x FETCH_SIZE KB (gfx950
+    reports half of a wide coalesced stream), write = WRITE_SIZE KB.  Runs
+    before this process touches the GPU; returns (bytes, note)."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir="/tmp")
+        cmd = [prof, "--pmc", counter, "--kernel-include-regex", "upols_process_kernel", "-d", d, "-o", "pmc",
+               "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--pmc-inner",
+               "--pmc", "off", "--no-cpu-baseline", "--steps", "20", "--warmup", "3",
+               "--channels", str(args.channels), "--block", str(args.block), "--ir", str(args.ir)]
+        try:
+            subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           timeout=240, check=True)
+        except Exception as e:  # no counters on this box: traffic stays null
+            return None, f"rocprofv3 --pmc {counter} failed: {type(e).__name__}"
+        got = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r.get("Counter_Name") == counter and "upols_process_kernel" in r.get("Kernel_Name", ""):
+                    got.append(float(r["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not got:
+            return None, f"no {counter} rows"
+        vals[counter] = statistics.median(got)
+    read_b = 2.0 * vals["FETCH_SIZE"] * 1024.0
+    write_b = vals["WRITE_SIZE"] * 1024.0
+    return int(read_b + write_b), (f"rocprofv3 --pmc, median of 20 launches per pass: read 2xFETCH_SIZE = "
+                                   f"{read_b / 1e6:.1f} MB, write WRITE_SIZE = {write_b / 1e6:.1f} MB")
+
+
+def make_irs(rank: int, C: int, L: int, world: int = 1) -> np.ndarray:
+    """Distinct IR per global channel (fftconv_amd.shard.synth_irs)."""
+    from fftconv_amd import shard
+
+    return shard.synth_irs(shard.channel_range(rank, max(world, rank + 1), C), L)
 
 
 def cpu_baseline(C: int, B: int, L: int, target_s: float):
@@ -109,6 +151,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and world > 1:
         args.gpus = world
+    traffic, traffic_note = None, "not collected (N>1 or --pmc off)"
+    if args.pmc == "auto" and world == 1 and not args.pmc_inner:
+        traffic, traffic_note = pmc_traffic(args)  # child processes, before this one touches the GPU
 
     import torch
 
@@ -122,21 +167,22 @@ def main():
 
     import fftconv_amd as F
 
+    from fftconv_amd import shard
+
     C, B, L = args.channels, args.block, args.ir
-    irs = make_irs(rank, C, L)
+    mine = shard.channel_range(rank, world, C)  # global channel ids of this rank
+    irs = shard.synth_irs(mine, L)
     conv = F.FFTConvolver.init(irs, B, L, channels=C, device=local_rank)
     del irs
     S = conv.seg_count
     ring = max(1, args.ring)
-    g = torch.Generator(device=dev)
-    g.manual_seed(4321 + rank)
     if args.dry == "shared":
-        dry = torch.empty((ring, B), device=dev)
-        if rank == 0:
-            dry.uniform_(-1.0, 1.0, generator=g)
+        dry = torch.from_numpy(shard.synth_shared_dry(ring, B)).to(dev)
+        if rank != 0:
+            dry.zero_()  # rank 0 owns the source; the others receive it by broadcast
         xin = None
     else:
-        xin = torch.empty((ring, C, B), device=dev).uniform_(-1.0, 1.0, generator=g)
+        xin = torch.from_numpy(shard.synth_dry(mine, ring, B)).to(dev)
     yout = torch.empty((ring, C, B), device=dev)
     # a dedicated stream: torch's default stream is the NULL handle, which the
     # C ABI reads as "the handle's own stream"
@@ -150,7 +196,7 @@ def main():
         if args.dry == "shared":
             d = dry[r]
             if dist is not None:
-                dist.broadcast(d, src=0)
+                shard.broadcast_dry(dist, d, src=0)
             # every channel reads the same broadcast block (input stride 0)
             conv.process_device(d.data_ptr(), 0, yout[r].data_ptr(), B, B, sh)
         else:
@@ -190,13 +236,9 @@ def main():
     per_launch_s = kern_ms / 1000.0 / args.steps
     bytes_per_launch = algorithmic_bytes_per_channel_block(B, L) * C
     achieved = bytes_per_launch / per_launch_s / 1e9
-    traffic = None
-    if args.traffic and os.path.exists(args.traffic):
-        try:
-            traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
 
+    if rank == 0 and args.pmc_inner:
+        return
     if rank == 0:
         cpu = None
         if args.gpus == 1 and not args.no_cpu_baseline:
@@ -232,6 +274,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_note": traffic_note,
+                "traffic_gbs": round(traffic / per_launch_s / 1e9, 1) if traffic else None,
                 "kernel": "upols_process_kernel (fused UPOLS step, one workgroup per channel)",
                 "bytes_per_launch": bytes_per_launch,
                 "launch_us": round(per_launch_s * 1e6, 3),

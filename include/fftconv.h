@@ -59,8 +59,9 @@ int fftconv_device_count(void);                   /* visible HIP devices, 0 if n
 size_t fftconv_complex_size(size_t size);         /* src/fft_convolver.rs:66-68 */
 size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /* :534-540 */
 /* Tuning knob (process-wide): spectral-MAC scan variant of the fused kernel,
- * -1 = automatic (default: nontemporal + zig-zag when the per-step H+X
- * stream exceeds the Infinity Cache, plain loads otherwise), else bit 0 =
+ * -1 = automatic (default: nontemporal loads when the per-step H+X stream
+ * exceeds the Infinity Cache, plain loads otherwise -- bit-identical
+ * arithmetic either way), else bit 0 =
  * zig-zag segment order on alternate blocks, bit 1 = nontemporal H/X loads.
  * Results agree within f32 rounding across variants. */
 int fftconv_set_kernel_variant(int variant);

@@ -201,6 +201,42 @@ def test_uniform_kernel_variants(amd, oracle_mod, variant):
         amd.set_kernel_variant(-1)
 
 
+def test_load_policy_is_bit_identical(amd):
+    """Plain and nontemporal loads (the automatic choice) give the same bits."""
+    rng = np.random.default_rng(50)
+    C, B, L = 4, 256, 4000
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    outs = []
+    for v in (0, 2):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+            r = np.random.default_rng(51)
+            outs.append(np.concatenate([conv.process(np.stack([white(r, B) for _ in range(C)]))
+                                        for _ in range(30)], axis=1))
+        finally:
+            amd.set_kernel_variant(-1)
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_channel_shards_bitwise_equal_on_device(amd):
+    """Two channel shards reproduce the one-batch run bit for bit (the
+    multi-GPU path has no data-path exchange)."""
+    from fftconv_amd import shard
+
+    C, B, L, NB = 64, 256, 6000, 40
+    full = range(C)
+    irs = shard.synth_irs(full, L)
+    dry = shard.synth_dry(full, NB, B)
+    one = amd.FFTConvolver.init(irs, B, L, channels=C)
+    parts = [shard.split_channels(C, 2, r) for r in range(2)]
+    halves = [amd.FFTConvolver.init(irs[p.start:p.stop], B, L, channels=len(p)) for p in parts]
+    for b in range(NB):
+        y = one.process(dry[b])
+        ys = [h.process(dry[b][p.start:p.stop]) for h, p in zip(halves, parts)]
+        assert np.array_equal(y, np.concatenate(ys)), b
+
+
 def test_uniform_batch_distinct_channels(amd, oracle_mod):
     rng = np.random.default_rng(5)
     C, B, L = 8, 256, 3000
