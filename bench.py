@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--pmc", choices=["auto", "off"], default="auto",
                    help="collect HBM traffic with two rocprofv3 --pmc child passes (N=1, rank 0)")
     p.add_argument("--pmc-inner", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    p.add_argument("--same-device", action="store_true",
+                   help="debug: every rank on device 0 (rehearse the N>1 path on a one-GPU box, gloo)")
     return p.parse_args()
 
 
@@ -157,13 +160,18 @@ def main():
 
     import torch
 
+    if args.same_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     import fftconv_amd as F
 

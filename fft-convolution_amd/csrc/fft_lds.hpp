@@ -25,12 +25,15 @@ namespace fftconv {
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// Complex products with explicit fused multiply-adds.  The kernels are built
+// with -ffp-contract=off, so every rounding is spelled out here and every
+// instantiation (load policy, block size, shard size) computes the same bits.
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+    return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
 }
 // a * conj(w)
 __device__ __forceinline__ float2 cmulc(float2 a, float2 w) {
-    return make_float2(a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y);
+    return make_float2(fmaf(a.x, w.x, a.y * w.y), fmaf(a.y, w.x, -(a.x * w.y)));
 }
 template <bool INV>
 __device__ __forceinline__ float2 twmul(float2 a, float2 w) { return INV ? cmulc(a, w) : cmul(a, w); }

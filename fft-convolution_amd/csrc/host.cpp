@@ -755,7 +755,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant >= 0 && (variant & 0xff) > 3) return fail(FFTCONV_E_INVALID, "variant bits must be 0..3 (or -1 = auto)");
+    if (variant > 3) return fail(FFTCONV_E_INVALID, "variant must be 0..3 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }

@@ -33,7 +33,7 @@ struct Geo {
     static constexpr int F = B / VEC;                   // slots per row
     static constexpr int G = F >= NT ? 1 : NT / F;      // row groups (segment split)
     static constexpr int SPT = F >= NT ? F / NT : 1;    // slots per thread
-    static constexpr int U = SPT >= 8 ? 1 : 8 / SPT;    // rows in flight per thread
+    static constexpr int U = SPT == 1 ? 8 : (SPT == 2 ? 2 : 1);  // rows in flight per thread
     static constexpr size_t red_bytes = G > 1 ? (size_t)NT * VEC * sizeof(float2) : 0;
     static constexpr size_t lds_bytes = 2 * (size_t)B * sizeof(float2) + red_bytes + 16;
 };
@@ -50,12 +50,12 @@ struct Acc2 {
     float dc, ny;
     __device__ __forceinline__ void zero() { a = make_float4(0.f, 0.f, 0.f, 0.f); dc = ny = 0.f; }
     __device__ __forceinline__ void mac(float4 h, float4 x) {
-        a.x += h.x * x.x - h.y * x.y;
-        a.y += h.x * x.y + h.y * x.x;
-        a.z += h.z * x.z - h.w * x.w;
-        a.w += h.z * x.w + h.w * x.z;
-        dc += h.x * x.x;
-        ny += h.y * x.y;
+        a.x = fmaf(-h.y, x.y, fmaf(h.x, x.x, a.x));
+        a.y = fmaf(h.y, x.x, fmaf(h.x, x.y, a.y));
+        a.z = fmaf(-h.w, x.w, fmaf(h.z, x.z, a.z));
+        a.w = fmaf(h.w, x.z, fmaf(h.z, x.w, a.w));
+        dc = fmaf(h.x, x.x, dc);
+        ny = fmaf(h.y, x.y, ny);
     }
     __device__ __forceinline__ float4 get(int slot) const {
         return slot == 0 ? make_float4(dc, ny, a.z, a.w) : a;
@@ -64,7 +64,7 @@ struct Acc2 {
 struct Acc1 {  // B == 1: the only bin pair is (DC, Nyquist)
     float2 a;
     __device__ __forceinline__ void zero() { a = make_float2(0.f, 0.f); }
-    __device__ __forceinline__ void mac(float2 h, float2 x) { a.x += h.x * x.x; a.y += h.y * x.y; }
+    __device__ __forceinline__ void mac(float2 h, float2 x) { a.x = fmaf(h.x, x.x, a.x); a.y = fmaf(h.y, x.y, a.y); }
     __device__ __forceinline__ float2 get(int) const { return a; }
 };
 template <int VEC> using AccT = std::conditional_t<VEC == 2, Acc2, Acc1>;
@@ -72,47 +72,58 @@ template <int VEC> using AccT = std::conditional_t<VEC == 2, Acc2, Acc1>;
 __device__ __forceinline__ float4 vadd(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 __device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 
-// 16-/8-byte loads of the H / X streams; NTL = nontemporal (streamed once per step)
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef float f2v __attribute__((ext_vector_type(2)));
-template <bool NTL>
-__device__ __forceinline__ float4 ldv(const float4 *p) {
-    if constexpr (NTL) {
-        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
-        return make_float4(v.x, v.y, v.z, v.w);
-    } else {
-        return *p;
-    }
-}
-template <bool NTL>
-__device__ __forceinline__ float2 ldv(const float2 *p) {
-    if constexpr (NTL) {
-        const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v *>(p));
-        return make_float2(v.x, v.y);
-    } else {
-        return *p;
-    }
-}
-
 // conv = pre + x (.) h for one slot, packed-aware (slot 0 bin 0 is (DC, Nyquist)).
 __device__ __forceinline__ float4 slot_mac(float4 pre, float4 x, float4 h, int slot) {
     float4 r;
     if (slot == 0) {
-        r.x = pre.x + x.x * h.x;
-        r.y = pre.y + x.y * h.y;
+        r.x = fmaf(x.x, h.x, pre.x);
+        r.y = fmaf(x.y, h.y, pre.y);
     } else {
-        r.x = pre.x + (x.x * h.x - x.y * h.y);
-        r.y = pre.y + (x.x * h.y + x.y * h.x);
+        r.x = fmaf(-x.y, h.y, fmaf(x.x, h.x, pre.x));
+        r.y = fmaf(x.y, h.x, fmaf(x.x, h.y, pre.y));
     }
-    r.z = pre.z + (x.z * h.z - x.w * h.w);
-    r.w = pre.w + (x.z * h.w + x.w * h.z);
+    r.z = fmaf(-x.w, h.w, fmaf(x.z, h.z, pre.z));
+    r.w = fmaf(x.w, h.z, fmaf(x.z, h.w, pre.w));
     return r;
 }
 __device__ __forceinline__ float2 slot_mac(float2 pre, float2 x, float2 h, int) {
-    return make_float2(pre.x + x.x * h.x, pre.y + x.y * h.y);
+    return make_float2(fmaf(x.x, h.x, pre.x), fmaf(x.y, h.y, pre.y));
 }
 __device__ __forceinline__ bool slot0_finite(float4 v) { return isfinite(v.x) && isfinite(v.y); }
 __device__ __forceinline__ bool slot0_finite(float2 v) { return isfinite(v.x) && isfinite(v.y); }
+
+// Buffer-resource streams (guide T8): one wave-uniform descriptor per channel
+// stream, the row offset in an SGPR (soffset) when the row is wave-uniform,
+// one shared per-lane voffset -- no per-load 64-bit address registers.
+// aux 2 = nontemporal.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+struct RowStream {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ RowStream(const float2 *base, size_t bytes) {
+        r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2 *>(base), 0, (int)bytes, 0x00020000);
+    }
+    // (an explicitly typed vector + memcpy: indexing the builtin's result
+    // through __builtin_bit_cast made hipcc emit a single-dword load)
+    template <bool NTL>
+    __device__ __forceinline__ float4 ld4(int voff, int soff) const {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, NTL ? 2 : 0);
+        float4 f;
+        __builtin_memcpy(&f, &v, sizeof(f));
+        return f;
+    }
+    template <bool NTL>
+    __device__ __forceinline__ float2 ld2(int voff, int soff) const {
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, NTL ? 2 : 0);
+        float2 f;
+        __builtin_memcpy(&f, &v, sizeof(f));
+        return f;
+    }
+    template <bool NTL>
+    __device__ __forceinline__ float4 ld(int voff, int soff, float4 *) const { return ld4<NTL>(voff, soff); }
+    template <bool NTL>
+    __device__ __forceinline__ float2 ld(int voff, int soff, float2 *) const { return ld2<NTL>(voff, soff); }
+};
 
 // pre_multiplied = sum_{i=1}^{act-1} H[i] (.) X[(cur+i) % act] over this
 // thread's slots (src/fft_convolver.rs:258-269).  Rows i = 1..act-1 are
@@ -120,11 +131,16 @@ __device__ __forceinline__ bool slot0_finite(float2 v) { return isfinite(v.x) &&
 // ZZ: every other block scans the rows backwards (rows read last by one step
 // are read first by the next).  NTL: nontemporal loads.
 template <int LOG2B, int NT, bool ZZ, bool NTL, class AccArr>
-__device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const float2 *Xc, int cur, int act,
+__device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const float2 *Xc, int S, int cur, int act,
                                          int flags, int f0, int g) {
     using Gm = Geo<LOG2B, NT>;
-    constexpr int B = Gm::B, VEC = Gm::VEC, G = Gm::G, SPT = Gm::SPT, U = Gm::U;
+    constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT, U = Gm::U;
+    constexpr int ROWB = B * (int)sizeof(float2);  // bytes per row
+    constexpr bool UNIFORM = F >= 64;              // a row group spans whole waves
     using vec_t = typename VecT<VEC>::type;
+    const size_t bytes = (size_t)S * ROWB;
+    const RowStream hs(Hc, bytes), xs(Xc, bytes);
+    const int lane_off = f0 * VEC * (int)sizeof(float2);
 #pragma unroll
     for (int s = 0; s < SPT; ++s) acc[s].zero();
     const bool rev = ZZ && (flags & FLAG_REV);
@@ -136,12 +152,12 @@ __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const fl
         vec_t hv[U][SPT], xv[U][SPT];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)i * B);
-            const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xi * B);
+            const int ho = i * ROWB, xo = xi * ROWB;
 #pragma unroll
             for (int s = 0; s < SPT; ++s) {
-                hv[u][s] = ldv<NTL>(hrow + f0 + s * NT);
-                xv[u][s] = ldv<NTL>(xrow + f0 + s * NT);
+                const int lo = lane_off + s * NT * VEC * (int)sizeof(float2);
+                hv[u][s] = UNIFORM ? hs.ld<NTL>(lo, ho, (vec_t *)nullptr) : hs.ld<NTL>(lo + ho, 0, (vec_t *)nullptr);
+                xv[u][s] = UNIFORM ? xs.ld<NTL>(lo, xo, (vec_t *)nullptr) : xs.ld<NTL>(lo + xo, 0, (vec_t *)nullptr);
             }
             i += di;
             xi += di;
@@ -154,11 +170,14 @@ __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const fl
             for (int s = 0; s < SPT; ++s) acc[s].mac(hv[u][s], xv[u][s]);
     }
     for (; t < act - 1; t += G) {
-        const vec_t *hrow = reinterpret_cast<const vec_t *>(Hc + (size_t)i * B);
-        const vec_t *xrow = reinterpret_cast<const vec_t *>(Xc + (size_t)xi * B);
+        const int ho = i * ROWB, xo = xi * ROWB;
 #pragma unroll
-        for (int s = 0; s < SPT; ++s)
-            acc[s].mac(ldv<NTL>(hrow + f0 + s * NT), ldv<NTL>(xrow + f0 + s * NT));
+        for (int s = 0; s < SPT; ++s) {
+            const int lo = lane_off + s * NT * VEC * (int)sizeof(float2);
+            const vec_t h = UNIFORM ? hs.ld<NTL>(lo, ho, (vec_t *)nullptr) : hs.ld<NTL>(lo + ho, 0, (vec_t *)nullptr);
+            const vec_t x = UNIFORM ? xs.ld<NTL>(lo, xo, (vec_t *)nullptr) : xs.ld<NTL>(lo + xo, 0, (vec_t *)nullptr);
+            acc[s].mac(h, x);
+        }
         i += di;
         xi += di;
         if (xi >= act) xi -= act;
@@ -171,7 +190,7 @@ __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const fl
 // one channel per workgroup, the whole chunk loop of one call on device.
 // ---------------------------------------------------------------------------
 template <int LOG2B, int NT, bool ZZ, bool NTL>
-__global__ __launch_bounds__(NT) void upols_process_kernel(ProcArgs a) {
+__global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
     using Gm = Geo<LOG2B, NT>;
     constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT;
     constexpr float invN = 1.0f / (float)(2 * B);
@@ -210,7 +229,9 @@ __global__ __launch_bounds__(NT) void upols_process_kernel(ProcArgs a) {
     // slot ownership: the MAC splits rows over G groups; the owner of slot f
     // after the reduction is thread f (G > 1) or thread f % NT (G == 1).
     const int f0 = G > 1 ? tid % F : tid;
-    const int g = G > 1 ? tid / F : 0;
+    // a row group spans whole waves when F >= 64: make g wave-uniform so the
+    // row walk (i, xi, row addresses) lives in scalar registers
+    const int g = G > 1 ? (F >= 64 ? __builtin_amdgcn_readfirstlane(tid / F) : tid / F) : 0;
     const bool owner = G > 1 ? tid < F : true;
 
     vec_t pacc[SPT];
@@ -227,12 +248,7 @@ __global__ __launch_bounds__(NT) void upols_process_kernel(ProcArgs a) {
 
         if (was_empty) {                                                 // :258-269
             AccT<VEC> acc[SPT];
-            // hot channels (index < a.hot) stream with plain loads so they can
-            // stay resident in the Infinity Cache; the rest stream nontemporally
-            if (NTL && (int)c >= a.hot)
-                mac_rows<LOG2B, NT, ZZ, true>(acc, Hc, Xc, cur, act, flags, f0, g);
-            else
-                mac_rows<LOG2B, NT, ZZ, false>(acc, Hc, Xc, cur, act, flags, f0, g);
+            mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, a.S, cur, act, flags, f0, g);
             if constexpr (G > 1) {
                 red[g * F + f0] = acc[0].get(f0);
                 __syncthreads();
@@ -453,8 +469,11 @@ __global__ void reset_state_kernel(int4 *state, int channels) {
 // ---------------------------------------------------------------------------
 constexpr int kNT = 256;
 
+// threads per workgroup of the fused kernel: 256 up to B = 1024; larger
+// blocks get more lanes so each owns <= 4 slots (no spills at 4 waves/SIMD)
+constexpr int proc_nt(int log2b) { return log2b <= 10 ? 256 : (log2b == 11 ? 512 : 1024); }
+
 static int g_variant = VARIANT_AUTO;
-static int g_hot = 0;
 
 // Automatic variant: a per-step H+X stream larger than the 256 MiB Infinity
 // Cache is re-read from HBM every step whatever the load policy, and there
@@ -472,12 +491,13 @@ static int pick_variant(const ProcArgs &a, int channels, int log2b) {
 
 template <int LOG2B>
 static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t s) {
-    using Gm = Geo<LOG2B, kNT>;
-    auto kern = upols_process_kernel<LOG2B, kNT, false, false>;
+    constexpr int PNT = proc_nt(LOG2B);
+    using Gm = Geo<LOG2B, PNT>;
+    auto kern = upols_process_kernel<LOG2B, PNT, false, false>;
     switch (pick_variant(a, channels, LOG2B) & 3) {
-        case 1: kern = upols_process_kernel<LOG2B, kNT, true, false>; break;
-        case 2: kern = upols_process_kernel<LOG2B, kNT, false, true>; break;
-        case 3: kern = upols_process_kernel<LOG2B, kNT, true, true>; break;
+        case 1: kern = upols_process_kernel<LOG2B, PNT, true, false>; break;
+        case 2: kern = upols_process_kernel<LOG2B, PNT, false, true>; break;
+        case 3: kern = upols_process_kernel<LOG2B, PNT, true, true>; break;
         default: break;
     }
     if (Gm::lds_bytes > 64 * 1024) {
@@ -485,9 +505,7 @@ static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t 
                                            (int)Gm::lds_bytes);
         if (e != hipSuccess) return e;
     }
-    ProcArgs b = a;
-    b.hot = g_hot;
-    hipLaunchKernelGGL(kern, dim3(channels), dim3(kNT), Gm::lds_bytes, s, b);
+    hipLaunchKernelGGL(kern, dim3(channels), dim3(PNT), Gm::lds_bytes, s, a);
     return hipGetLastError();
 }
 
@@ -544,11 +562,8 @@ hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStre
     return hipGetLastError();
 }
 
-void set_variant(int v) {
-    g_variant = v < 0 ? VARIANT_AUTO : (v & 0xff);
-    g_hot = v < 0 ? 0 : v >> 8;
-}
-int get_variant() { return g_variant == VARIANT_AUTO ? -1 : (g_variant | (g_hot << 8)); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 3); }
+int get_variant() { return g_variant == VARIANT_AUTO ? -1 : g_variant; }
 
 hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;
@@ -558,7 +573,7 @@ hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s) {
 
 size_t process_lds_bytes(int log2b) {
     switch (log2b) {
-#define LDSCASE(L) case L: return Geo<L, kNT>::lds_bytes;
+#define LDSCASE(L) case L: return Geo<L, proc_nt(L)>::lds_bytes;
         LDSCASE(0) LDSCASE(1) LDSCASE(2) LDSCASE(3) LDSCASE(4) LDSCASE(5) LDSCASE(6)
         LDSCASE(7) LDSCASE(8) LDSCASE(9) LDSCASE(10) LDSCASE(11) LDSCASE(12) LDSCASE(13)
 #undef LDSCASE

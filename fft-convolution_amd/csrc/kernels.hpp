@@ -29,7 +29,6 @@ struct ProcArgs {
     const float2 *tw;      // W_N^k, k < N = 2B
     int S;                 // seg_count (row pitch of H and X in rows)
     int n;                 // output samples this call
-    int hot;               // channels [0, hot) use cache-allocating loads (NT variants)
 };
 
 struct IrArgs {
