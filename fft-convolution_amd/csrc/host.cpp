@@ -259,13 +259,21 @@ struct UniformCore {
         return FFTCONV_OK;
     }
 
+    ProcJob job(const float *din, size_t is, float *dout, size_t os, size_t n) const {
+        ProcJob j{};
+        j.H = H.p; j.X = X.p; j.overlap = overlap.p; j.inbuf = inbuf.p; j.pre = pre.p; j.state = state.p;
+        j.in = din; j.in_stride = (long long)is; j.out = dout; j.out_stride = (long long)os;
+        j.S = (int)S; j.n = (int)n;
+        return j;
+    }
+
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t n, hipStream_t s) {
         if (n > (size_t)INT32_MAX) return fail(FFTCONV_E_UNSUPPORTED, "process length exceeds 2^31-1");
         if (n == 0 || C == 0) return FFTCONV_OK;
         ProcArgs a{};
-        a.H = H.p; a.X = X.p; a.overlap = overlap.p; a.inbuf = inbuf.p; a.pre = pre.p; a.state = state.p;
-        a.in = din; a.in_stride = (long long)is; a.out = dout; a.out_stride = (long long)os;
-        a.tw = tw.p; a.S = (int)S; a.n = (int)n;
+        a.job[0] = job(din, is, dout, os, n);
+        a.tw = tw.p;
+        a.njobs = 1;
         HIP_TRY(launch_process(log2b, a, (int)C, s));
         return FFTCONV_OK;
     }
@@ -326,28 +334,42 @@ struct TwoStageCore {
     int device = 0;
     size_t C = 0, head_bs = 0, T = 0;
     std::unique_ptr<UniformCore> head, tail0, tail;  // null tail = Default (zeros)
-    DevPtr<float> out0, pre0, out1, pre1, tin;      // [C][T] each
+    DevPtr<float> out0, pre0, out1, pre1;            // [C][T] each
+    DevPtr<float> tin_buf[2];                        // tail_input, double-buffered per tail period
+    int tin_idx = 0;
     float *tail_output0 = nullptr, *tail_precalculated0 = nullptr;
     float *tail_output = nullptr, *tail_precalculated = nullptr;
     size_t tail_input_fill = 0, precalculated_pos = 0;
     hipStream_t stream = nullptr;
+    // The T-sized tail convolution runs on its own stream: its result is first
+    // read one whole tail period later (after the next swap), which is the
+    // reference's "might be done in some background thread" (:492).
+    hipStream_t side = nullptr;
+    hipEvent_t ev_main = nullptr, ev_tail = nullptr;
+    bool tail_in_flight = false;
     Scratch scratch;
 
     ~TwoStageCore() {
-        if (stream) {
-            DeviceGuard g(device);
-            (void)hipStreamSynchronize(stream);
-            (void)hipStreamDestroy(stream);
-        }
+        DeviceGuard g(device);
+        if (side) { (void)hipStreamSynchronize(side); (void)hipStreamDestroy(side); }
+        if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
+        if (ev_main) (void)hipEventDestroy(ev_main);
+        if (ev_tail) (void)hipEventDestroy(ev_tail);
     }
 
+    float *tail_input() const { return tin_buf[tin_idx].p; }
+
     int alloc_buffers() {
-        for (auto *b : {&out0, &pre0, &out1, &pre1, &tin}) {
+        HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming));
+        for (auto *b : {&out0, &pre0, &out1, &pre1, &tin_buf[0], &tin_buf[1]}) {
             if (int r = b->alloc(C * T)) return r;
             if (b->n) HIP_TRY(hipMemsetAsync(b->p, 0, b->bytes(), stream));
         }
         tail_output0 = out0.p; tail_precalculated0 = pre0.p;
         tail_output = out1.p; tail_precalculated = pre1.p;
+        tin_idx = 0;
         return FFTCONV_OK;
     }
 
@@ -369,7 +391,6 @@ struct TwoStageCore {
         // are cut on the host so each stage sees exactly its reference slice
         const size_t sstride = stride == 0 ? 0 : stride;
         auto slice = [&](size_t off, size_t cnt, std::vector<float> &buf) -> size_t {
-            // rows of `cnt` samples starting at padded_ir[off]; returns the row stride used
             const size_t rows = (sstride == 0) ? 1 : C;
             buf.assign(rows * std::max<size_t>(cnt, 1), 0.f);
             for (size_t c = 0; c < rows; ++c)
@@ -404,9 +425,55 @@ struct TwoStageCore {
         return FFTCONV_OK;
     }
 
+    // fill reached T (:478-505): swap the tail0 buffers, swap the tail buffers,
+    // and start the tail convolution of this period on the side stream.
+    int end_of_period(hipStream_t s) {
+        std::swap(tail_precalculated0, tail_output0);                         // :487-489
+        std::swap(tail_precalculated, tail_output);                           // :497
+        // work after this point reads the swapped-in tail_precalculated: it is
+        // the previous period's tail result, so wait for that kernel here
+        if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(s, ev_tail, 0));
+        if (tail) {                                                            // :498-499
+            HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
+            HIP_TRY(hipStreamWaitEvent(side, ev_main, 0));
+            if (int r = tail->process_device(tail_input(), T, tail_output, T, T, side)) return r;
+            HIP_TRY(hipEventRecord(ev_tail, side));
+            tail_in_flight = true;
+        }
+        tin_idx ^= 1;  // the next period fills the other buffer while the tail reads this one
+        tail_input_fill = 0;                                                   // :502-505
+        precalculated_pos = 0;
+        return FFTCONV_OK;
+    }
+
     // TwoStageFFTConvolver::process (:426-509)
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t len, hipStream_t s) {
         if (len > head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
+        if (len == 0 || C == 0) return FFTCONV_OK;
+        if (len == head_bs && tail_input_fill % head_bs == 0 && tail_input_fill + len <= T) {
+            // aligned call: one sub-chunk, and tail0 consumes exactly this block.
+            // One launch: head (+ the sub-chunk epilogue) and tail0 as two jobs.
+            ProcArgs a{};
+            a.job[0] = head->job(din, is, dout, os, len);                       // :431
+            a.job[0].add0 = tail_precalculated0 + precalculated_pos;            // :453-459
+            a.job[0].add1 = tail_precalculated + precalculated_pos;             // :462-468
+            a.job[0].add_stride = (long long)T;
+            a.job[0].tin = tail_input() + tail_input_fill;                     // :473-475
+            a.job[0].tin_stride = (long long)T;
+            a.njobs = 1;
+            if (tail0) {                                                        // :478-486
+                a.job[1] = tail0->job(din, is, tail_output0 + tail_input_fill, T, head_bs);
+                a.njobs = 2;
+            }
+            a.tw = head->tw.p;
+            HIP_TRY(launch_process(head->log2b, a, (int)C, s));
+            precalculated_pos += len;
+            tail_input_fill += len;
+            if (tail_input_fill == T) {
+                if (int r = end_of_period(s)) return r;
+            }
+            return FFTCONV_OK;
+        }
         if (int r = head->process_device(din, is, dout, os, len, s)) return r;   // :431
         size_t processed = 0;
         while (processed < len) {                                                 // :441
@@ -417,26 +484,17 @@ struct TwoStageCore {
             a.out = dout; a.out_stride = (long long)os;
             a.p0 = tail_precalculated0; a.p1 = tail_precalculated; a.T = (long long)T;
             a.pos = (int)precalculated_pos; a.in = din; a.in_stride = (long long)is;
-            a.sb = (int)processed; a.tail_input = tin.p; a.fill = (int)tail_input_fill; a.cnt = (int)processing;
+            a.sb = (int)processed; a.tail_input = tail_input(); a.fill = (int)tail_input_fill;
+            a.cnt = (int)processing;
             HIP_TRY(launch_twostage_accum(a, (int)C, s));                        // :452-475
             precalculated_pos += processing;
             tail_input_fill += processing;
-            if (tail_input_fill % head_bs == 0) {                                 // :478-490
+            if (tail_input_fill % head_bs == 0 && tail0) {                        // :478-486
                 const size_t off = tail_input_fill - head_bs;
-                if (tail0) {
-                    if (int r = tail0->process_device(tin.p + off, T, tail_output0 + off, T, head_bs, s)) return r;
-                }
-                if (tail_input_fill == T) std::swap(tail_precalculated0, tail_output0);
+                if (int r = tail0->process_device(tail_input() + off, T, tail_output0 + off, T, head_bs, s)) return r;
             }
-            if (tail_input_fill == T) {                                           // :493-500
-                std::swap(tail_precalculated, tail_output);
-                if (tail) {
-                    if (int r = tail->process_device(tin.p, T, tail_output, T, T, s)) return r;
-                }
-            }
-            if (tail_input_fill == T) {                                           // :502-505
-                tail_input_fill = 0;
-                precalculated_pos = 0;
+            if (tail_input_fill == T) {
+                if (int r = end_of_period(s)) return r;
             }
             processed += processing;
         }
@@ -462,10 +520,11 @@ struct TwoStageCore {
         if (int r = head->reset(stream)) return r;
         if (tail0) { if (int r = tail0->reset(stream)) return r; }
         if (tail) { if (int r = tail->reset(stream)) return r; }
-        for (auto *b : {&out0, &pre0, &out1, &pre1, &tin})
+        for (auto *b : {&out0, &pre0, &out1, &pre1, &tin_buf[0], &tin_buf[1]})
             if (b->n) HIP_TRY(hipMemsetAsync(b->p, 0, b->bytes(), stream));
         tail_input_fill = 0;
         precalculated_pos = 0;
+        tail_in_flight = false;
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -493,8 +552,10 @@ struct TwoStageCore {
         };
         tail_output0 = map(o.tail_output0); tail_precalculated0 = map(o.tail_precalculated0);
         tail_output = map(o.tail_output); tail_precalculated = map(o.tail_precalculated);
+        tin_idx = o.tin_idx;
         const std::pair<DevPtr<float> *, const DevPtr<float> *> pairs[] = {
-            {&out0, &o.out0}, {&pre0, &o.pre0}, {&out1, &o.out1}, {&pre1, &o.pre1}, {&tin, &o.tin}};
+            {&out0, &o.out0}, {&pre0, &o.pre0}, {&out1, &o.out1}, {&pre1, &o.pre1},
+            {&tin_buf[0], &o.tin_buf[0]}, {&tin_buf[1], &o.tin_buf[1]}};
         for (auto &pr : pairs)
             if (pr.second->n)
                 HIP_TRY(hipMemcpyAsync(pr.first->p, pr.second->p, pr.second->bytes(), hipMemcpyDeviceToDevice, stream));
@@ -639,6 +700,31 @@ struct CrossfadeCore {
             }
         }
         HIP_TRY(hipStreamSynchronize(stream));
+        response_pending = true;
+        return FFTCONV_OK;
+    }
+
+    // Convolution::update (:51-64) from device samples, stream-ordered
+    int update_device(const float *src, size_t len, size_t stride, hipStream_t s) {
+        if (!is_crossfading()) {
+            UniformCore &t = xf.target == 0 ? *b : *a;
+            if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
+            if (int r = swap_device(src, stride, len, s)) return r;
+            response_pending = false;
+            return FFTCONV_OK;
+        }
+        if (len > stored_len) return fail(FFTCONV_E_INVALID, "assertion failed: response_len <= self.stored_response.len()");
+        if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), s));
+        if (len) {
+            if (stride == 0 || C == 1) {
+                HIP_TRY(hipMemcpyAsync(stored.p, src, len * sizeof(float), hipMemcpyDeviceToDevice, s));
+                stored_stride = C == 1 ? stored_len : 0;
+            } else {
+                HIP_TRY(hipMemcpy2DAsync(stored.p, stored_len * sizeof(float), src, stride * sizeof(float),
+                                         len * sizeof(float), C, hipMemcpyDeviceToDevice, s));
+                stored_stride = stored_len;
+            }
+        }
         response_pending = true;
         return FFTCONV_OK;
     }
@@ -792,6 +878,12 @@ int fftconv_uniform_update_channel(fftconv_uniform *h, size_t channel, const flo
     if (channel >= h->core.C) return fail(FFTCONV_E_INVALID, "channel out of range");
     return h->core.update_host(channel, 1, response, len, 0);
 }
+int fftconv_uniform_update_device(fftconv_uniform *h, const float *d_responses, size_t len, size_t stride,
+                                  void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    return h->core.update_device(d_responses, h->core.C == 1 ? 0 : stride, len, pick(hip_stream, h->core.stream));
+}
 int fftconv_uniform_reset(fftconv_uniform *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
@@ -914,6 +1006,12 @@ int fftconv_crossfade_update(fftconv_crossfade *h, const float *response, size_t
 int fftconv_crossfade_update_batch(fftconv_crossfade *h, const float *responses, size_t len, size_t stride) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     return h->core.update_host(responses, len, h->core.C == 1 ? 0 : stride);
+}
+int fftconv_crossfade_update_device(fftconv_crossfade *h, const float *d_responses, size_t len, size_t stride,
+                                    void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    return h->core.update_device(d_responses, len, h->core.C == 1 ? 0 : stride, pick(hip_stream, h->core.stream));
 }
 int fftconv_crossfade_reset(fftconv_crossfade *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");

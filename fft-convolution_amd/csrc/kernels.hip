@@ -35,7 +35,12 @@ struct Geo {
     static constexpr int SPT = F >= NT ? F / NT : 1;    // slots per thread
     static constexpr int U = SPT == 1 ? 8 : (SPT == 2 ? 2 : 1);  // rows in flight per thread
     static constexpr size_t red_bytes = G > 1 ? (size_t)NT * VEC * sizeof(float2) : 0;
-    static constexpr size_t lds_bytes = 2 * (size_t)B * sizeof(float2) + red_bytes + 16;
+    // B <= 512: the prologue stages by LDS-DMA the twiddle table (2B float2),
+    // H[0] (B float2), overlap, and the two tail slices (B floats each)
+    static constexpr bool PREFETCH = LOG2B <= 9;
+    static constexpr size_t tw_bytes = PREFETCH ? 2 * (size_t)B * sizeof(float2) : 0;
+    static constexpr size_t pre_bytes = PREFETCH ? (size_t)B * sizeof(float2) + 3 * (size_t)B * sizeof(float) : 0;
+    static constexpr size_t lds_bytes = ((2 * (size_t)B * sizeof(float2) + red_bytes + tw_bytes + pre_bytes + 15) / 16) * 16 + 16;
 };
 
 template <int VEC> struct VecT;
@@ -185,9 +190,59 @@ __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const fl
     }
 }
 
+// Asynchronous global -> LDS copies (LDS-DMA, global_load_lds): lane l of a
+// wave writes dst + l*W for a wave-uniform dst, no VGPR destination, drained
+// by the next __syncthreads (s_waitcnt vmcnt(0) before s_barrier).
+typedef __attribute__((address_space(1))) const void *gptr_t;
+typedef __attribute__((address_space(3))) void *lptr_t;
+template <int NT>
+__device__ __forceinline__ void dma_f32(float *dst, const float *src, int count) {  // any alignment
+    const int lane = threadIdx.x & 63;
+    for (int base = (threadIdx.x >> 6) * 64; base < count; base += NT)
+        if (base + lane < count)
+            __builtin_amdgcn_global_load_lds((gptr_t)(src + base + lane), (lptr_t)(dst + base), 4, 0, 0);
+}
+template <int NT>
+__device__ __forceinline__ void dma_16b(void *dst, const void *src, int bytes) {  // 16-byte aligned, bytes % 16 == 0
+    const int lane = threadIdx.x & 63;
+    const char *s = static_cast<const char *>(src);
+    char *d = static_cast<char *>(dst);
+    for (int base = (threadIdx.x >> 6) * 1024; base < bytes; base += NT * 16)
+        if (base + lane * 16 < bytes)
+            __builtin_amdgcn_global_load_lds((gptr_t)(s + base + lane * 16), (lptr_t)(d + base), 16, 0, 0);
+}
+
+// TwoStageFFTConvolver::process sub-chunk (src/fft_convolver.rs:452-475) fused
+// into the head job: output += precalculated0, then += precalculated (two
+// separate adds, like the reference's two loops), and tail_input <- input.
+// Generic form: a pass over the finished output.
+template <int NT>
+__device__ __forceinline__ void twostage_epilogue(const ProcJob &J, size_t c, float *outc, const float *inc, int n) {
+    if (!J.add0 && !J.tin) return;
+    __syncthreads();  // outc[] was written by other threads of this workgroup
+    const float *p0 = J.add0 ? J.add0 + c * J.add_stride : nullptr;
+    const float *p1 = J.add1 ? J.add1 + c * J.add_stride : nullptr;
+    float *ti = J.tin ? J.tin + c * J.tin_stride : nullptr;
+    for (int j = threadIdx.x; j < n; j += NT) {
+        if (p0) {
+            float v = outc[j];
+            v += p0[j];
+            if (p1) v += p1[j];
+            outc[j] = v;
+        }
+        if (ti) ti[j] = inc[j];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Fused UPOLS step: FFTConvolver::process (src/fft_convolver.rs:229-309) for
 // one channel per workgroup, the whole chunk loop of one call on device.
+//
+// Latency structure: every load that does not depend on the MAC is issued in
+// the prologue, so its round trip overlaps the FDL stream -- the twiddle table
+// (into LDS), H[0], and for the common one-full-block call the input block,
+// the overlap and the two-stage tail slices.  After the MAC the FFT / C2R /
+// overlap-add tail then runs out of LDS and registers only.
 // ---------------------------------------------------------------------------
 template <int LOG2B, int NT, bool ZZ, bool NTL>
 __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
@@ -200,31 +255,32 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
     float2 *bufA = reinterpret_cast<float2 *>(smem);
     float2 *bufB = bufA + B;
     vec_t *red = reinterpret_cast<vec_t *>(bufB + B);
-    int &s_err = *reinterpret_cast<int *>(smem + 2 * (size_t)B * sizeof(float2) + Gm::red_bytes);
+    int &s_err = *reinterpret_cast<int *>(smem + Gm::lds_bytes - 16);
 
     const int tid = threadIdx.x;
     const size_t c = blockIdx.x;
-    const int4 st = a.state[c];
+    const ProcJob &J = a.job[blockIdx.y];
+    const int4 st = J.state[c];
     int cur = st.x;
     const int act = st.y;
     int fill = st.z;
     int flags = st.w;
-    float *outc = a.out + c * a.out_stride;
-    const float *inc = a.in + c * a.in_stride;
-    const int n = a.n;
+    float *outc = J.out + c * J.out_stride;
+    const float *inc = J.in + c * J.in_stride;
+    const int n = J.n;
 
     if (act == 0) {  // :230-233 -- zero output, state untouched
         for (int j = tid; j < n; j += NT) outc[j] = 0.f;
+        twostage_epilogue<NT>(J, c, outc, inc, n);
         return;
     }
 
-    const size_t rows = (size_t)a.S * B;
-    const float2 *Hc = a.H + c * rows;
-    float2 *Xc = a.X + c * rows;
-    float *ovc = a.overlap + c * B;
-    float *ibc = a.inbuf + c * B;
-    float2 *prec = a.pre + c * B;
-    const float2 *__restrict__ tw = a.tw;
+    const size_t rows = (size_t)J.S * B;
+    const float2 *Hc = J.H + c * rows;
+    float2 *Xc = J.X + c * rows;
+    float *ovc = J.overlap + c * B;
+    float *ibc = J.inbuf + c * B;
+    float2 *prec = J.pre + c * B;
 
     // slot ownership: the MAC splits rows over G groups; the owner of slot f
     // after the reduction is thread f (G > 1) or thread f % NT (G == 1).
@@ -233,6 +289,37 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
     // row walk (i, xi, row addresses) lives in scalar registers
     const int g = G > 1 ? (F >= 64 ? __builtin_amdgcn_readfirstlane(tid / F) : tid / F) : 0;
     const bool owner = G > 1 ? tid < F : true;
+
+    // ---- prologue: loads independent of the MAC ------------------------------
+    constexpr bool PF = Gm::PREFETCH;
+    float2 *twl = reinterpret_cast<float2 *>(smem + 2 * (size_t)B * sizeof(float2) + Gm::red_bytes);
+    float2 *h0l = twl + 2 * B;
+    float *ovl = reinterpret_cast<float *>(h0l + B);
+    float *p0l = ovl + B;
+    float *p1l = p0l + B;
+    // the common call: exactly one full block from an empty input buffer
+    const bool one_block = PF && fill == 0 && n == B && !(flags & FLAG_INBUF);
+    const bool epi = J.add0 != nullptr || J.tin != nullptr;
+    if constexpr (PF) {
+        dma_16b<NT>(twl, a.tw, 2 * B * (int)sizeof(float2));
+        if constexpr (B >= 2) dma_16b<NT>(h0l, Hc, B * (int)sizeof(float2));
+        else dma_f32<NT>(reinterpret_cast<float *>(h0l), reinterpret_cast<const float *>(Hc), 2 * B);
+        if (one_block) {
+            // the zero-padded block, packed z[m] = (x[2m], x[2m+1]): x[0..B) lands
+            // as raw floats in bufA[0..B/2), the padding half is zero
+            dma_f32<NT>(reinterpret_cast<float *>(bufA), inc, B);
+            if constexpr (B >= 2) {
+                for (int m = B / 2 + tid; m < B; m += NT) bufA[m] = make_float2(0.f, 0.f);
+            } else {
+                if (tid == 0) bufA[0].y = 0.f;  // x[1] is padding when B == 1
+            }
+            dma_f32<NT>(ovl, ovc, B);
+            if (J.add0) dma_f32<NT>(p0l, J.add0 + c * J.add_stride, B);
+            if (J.add1) dma_f32<NT>(p1l, J.add1 + c * J.add_stride, B);
+        }
+    }
+    const float2 *tw = PF ? twl : a.tw;
+    const float2 *h0g = PF ? h0l : Hc;
 
     vec_t pacc[SPT];
     if (fill != 0 && owner) {  // a partial block carries pre_multiplied over
@@ -248,7 +335,7 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
 
         if (was_empty) {                                                 // :258-269
             AccT<VEC> acc[SPT];
-            mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, a.S, cur, act, flags, f0, g);
+            mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, J.S, cur, act, flags, f0, g);
             if constexpr (G > 1) {
                 red[g * F + f0] = acc[0].get(f0);
                 __syncthreads();
@@ -266,18 +353,29 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
 
         // forward FFT of the zero-padded input buffer into segments[current]
         // (:243-255): x[i] = chunk sample, else the carried input buffer.
-        for (int m = tid; m < B; m += NT) {
-            float2 z = make_float2(0.f, 0.f);
-            const int i0 = 2 * m, i1 = 2 * m + 1;
-            if (i0 < B) {
-                z.x = (i0 >= fill && i0 < fill + k) ? inc[processed + i0 - fill]
-                                                     : ((flags & FLAG_INBUF) ? ibc[i0] : 0.f);
+        if (one_block) {
+            // the block is already in bufA (prologue DMA); two-stage: append it
+            // to tail_input from LDS (:473-475)
+            __syncthreads();
+            if (J.tin) {
+                const float *xb = reinterpret_cast<const float *>(bufA);
+                float *ti = J.tin + c * J.tin_stride;
+                for (int j = tid; j < B; j += NT) ti[j] = xb[j];
             }
-            if (i1 < B) {
-                z.y = (i1 >= fill && i1 < fill + k) ? inc[processed + i1 - fill]
-                                                     : ((flags & FLAG_INBUF) ? ibc[i1] : 0.f);
+        } else {
+            for (int m = tid; m < B; m += NT) {
+                float2 z = make_float2(0.f, 0.f);
+                const int i0 = 2 * m, i1 = 2 * m + 1;
+                if (i0 < B) {
+                    z.x = (i0 >= fill && i0 < fill + k) ? inc[processed + i0 - fill]
+                                                         : ((flags & FLAG_INBUF) ? ibc[i0] : 0.f);
+                }
+                if (i1 < B) {
+                    z.y = (i1 >= fill && i1 < fill + k) ? inc[processed + i1 - fill]
+                                                         : ((flags & FLAG_INBUF) ? ibc[i1] : 0.f);
+                }
+                bufA[m] = z;
             }
-            bufA[m] = z;
         }
         if (tid == 0) s_err = 0;
         __syncthreads();
@@ -293,13 +391,12 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
 
         // conv = pre_multiplied + segments[current] (.) segments_ir[0] (:270-275)
         if (owner) {
-            const vec_t *h0 = reinterpret_cast<const vec_t *>(Hc);
             const vec_t *q = reinterpret_cast<const vec_t *>(Q);
             vec_t *zc = reinterpret_cast<vec_t *>(Z);
 #pragma unroll
             for (int s = 0; s < SPT; ++s) {
                 const int f = f0 + s * NT;
-                const vec_t cv = slot_mac(pacc[s], q[f], h0[f], f);
+                const vec_t cv = slot_mac(pacc[s], q[f], reinterpret_cast<const vec_t *>(h0g)[f], f);
                 zc[f] = cv;
                 // realfft's C2R rejects a non-zero DC/Nyquist imaginary part,
                 // which only a non-finite operand can produce (:278-281)
@@ -316,10 +413,21 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
         const float *y = reinterpret_cast<const float *>(Y);
 
         // overlap-add (:284-288)
-        for (int j = tid; j < k; j += NT) outc[processed + j] = y[fill + j] * invN + ovc[fill + j];
+        if (one_block) {
+            for (int j = tid; j < B; j += NT) {
+                float v = y[j] * invN + ovl[j];
+                if (J.add0) {  // two-stage sub-chunk adds (:453-468), same rounding order
+                    v += p0l[j];
+                    if (J.add1) v += p1l[j];
+                }
+                outc[j] = v;
+            }
+        } else {
+            for (int j = tid; j < k; j += NT) outc[processed + j] = y[fill + j] * invN + ovc[fill + j];
+        }
         const bool complete = fill + k == B;                              // :291-292
         if (complete) {
-            __syncthreads();
+            if (!one_block) __syncthreads();  // every overlap read above is done
             for (int j = tid; j < B; j += NT) ovc[j] = y[B + j] * invN;  // :297-298
             if (flags & FLAG_INBUF)
                 for (int j = tid; j < B; j += NT) ibc[j] = 0.f;           // :294
@@ -348,7 +456,8 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
 #pragma unroll
         for (int s = 0; s < SPT; ++s) reinterpret_cast<vec_t *>(prec)[f0 + s * NT] = pacc[s];
     }
-    if (tid == 0) a.state[c] = make_int4(cur, act, fill, flags);
+    if (tid == 0) J.state[c] = make_int4(cur, act, fill, flags);
+    if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
 }
 
 // ---------------------------------------------------------------------------
@@ -485,7 +594,8 @@ static int g_variant = VARIANT_AUTO;
 // shards bit-identical whatever the shard size.
 static int pick_variant(const ProcArgs &a, int channels, int log2b) {
     if (g_variant != VARIANT_AUTO) return g_variant;
-    const double stream = 16.0 * (double)channels * (double)a.S * (double)(1 << log2b);
+    double stream = 0.0;
+    for (int j = 0; j < a.njobs; ++j) stream += 16.0 * (double)channels * (double)a.job[j].S * (double)(1 << log2b);
     return stream > 192.0 * 1024 * 1024 ? VARIANT_NT : 0;
 }
 
@@ -505,7 +615,7 @@ static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t 
                                            (int)Gm::lds_bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(channels), dim3(PNT), Gm::lds_bytes, s, a);
+    hipLaunchKernelGGL(kern, dim3(channels, a.njobs), dim3(PNT), Gm::lds_bytes, s, a);
     return hipGetLastError();
 }
 

@@ -15,7 +15,11 @@ enum : int { VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_AUTO = 0x7fffffff };
 void set_variant(int v);
 int get_variant();
 
-struct ProcArgs {
+// One convolver batch's call (FFTConvolver::process over `n` samples of every
+// channel), optionally with the two-stage epilogue of the head block
+// (src/fft_convolver.rs:452-475): out[j] += add0[j], then += add1[j], and
+// tin[j] = in[j], applied after the call.
+struct ProcJob {
     const float2 *H;       // [C][S][B] packed IR spectra
     float2 *X;             // [C][S][B] packed FDL
     float *overlap;        // [C][B]
@@ -26,9 +30,21 @@ struct ProcArgs {
     long long in_stride;
     float *out;
     long long out_stride;
-    const float2 *tw;      // W_N^k, k < N = 2B
+    const float *add0;     // tail_precalculated0 + precalculated_pos (or null)
+    const float *add1;     // tail_precalculated  + precalculated_pos (or null)
+    long long add_stride;
+    float *tin;            // tail_input + tail_input_fill (or null)
+    long long tin_stride;
     int S;                 // seg_count (row pitch of H and X in rows)
     int n;                 // output samples this call
+};
+
+// Up to two jobs of the same block size in one launch (grid.y = job): the
+// two-stage head and tail0 run together on the same input block.
+struct ProcArgs {
+    ProcJob job[2];
+    const float2 *tw;      // W_N^k, k < N = 2B
+    int njobs;
 };
 
 struct IrArgs {

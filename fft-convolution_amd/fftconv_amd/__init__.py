@@ -48,6 +48,7 @@ SIGNATURES = {
     "fftconv_uniform_update": (_i, [_vp, _fp, _sz]),
     "fftconv_uniform_update_batch": (_i, [_vp, _fp, _sz, _sz]),
     "fftconv_uniform_update_channel": (_i, [_vp, _sz, _fp, _sz]),
+    "fftconv_uniform_update_device": (_i, [_vp, _vp, _sz, _sz, _vp]),
     "fftconv_uniform_reset": (_i, [_vp]),
     "fftconv_uniform_process": (_i, [_vp, _fp, _sz, _fp, _sz]),
     "fftconv_uniform_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
@@ -73,6 +74,7 @@ SIGNATURES = {
     "fftconv_crossfade_new": (_vp, [_vp, _sz, _sz, _sz]),
     "fftconv_crossfade_update": (_i, [_vp, _fp, _sz]),
     "fftconv_crossfade_update_batch": (_i, [_vp, _fp, _sz, _sz]),
+    "fftconv_crossfade_update_device": (_i, [_vp, _vp, _sz, _sz, _vp]),
     "fftconv_crossfade_reset": (_i, [_vp]),
     "fftconv_crossfade_process": (_i, [_vp, _fp, _sz, _fp, _sz]),
     "fftconv_crossfade_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
@@ -239,6 +241,12 @@ class FFTConvolver(_Base):
         else:
             _check(lib().fftconv_uniform_update(self._h, _p(r), r.size))
 
+    def update_device(self, d_responses: int, response_len: int, stride: int = 0, stream: int = 0):
+        """update() from device memory (channel c at d_responses + 4*c*stride;
+        stride 0 = same response for all channels), stream-ordered."""
+        _check(self._fn("update_device")(self._h, C.c_void_p(d_responses), response_len, stride,
+                                         C.c_void_p(stream) if stream else None))
+
     def update_channel(self, channel: int, response):
         r = _f32(response)
         _check(lib().fftconv_uniform_update_channel(self._h, channel, _p(r), r.size))
@@ -329,6 +337,12 @@ class CrossfadeConvolver(_Base):
             _check(lib().fftconv_crossfade_update_batch(self._h, _p(r), r.shape[1], r.shape[1]))
         else:
             _check(lib().fftconv_crossfade_update(self._h, _p(r), r.size))
+
+    def update_device(self, d_responses: int, response_len: int, stride: int = 0, stream: int = 0):
+        """update() from device memory (channel c at d_responses + 4*c*stride;
+        stride 0 = same response for all channels), stream-ordered."""
+        _check(self._fn("update_device")(self._h, C.c_void_p(d_responses), response_len, stride,
+                                         C.c_void_p(stream) if stream else None))
 
     def reset(self):
         _check(lib().fftconv_crossfade_reset(self._h))

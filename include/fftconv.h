@@ -85,6 +85,11 @@ int fftconv_uniform_update_batch(fftconv_uniform *h, const float *responses, siz
 /* One channel only. */
 int fftconv_uniform_update_channel(fftconv_uniform *h, size_t channel, const float *response,
                                    size_t response_len);
+/* update() from device-resident responses (channel c at d_responses[c*stride],
+ * stride 0 = one response for every channel), enqueued on `hip_stream`
+ * (NULL = own stream) without a host synchronisation or an allocation. */
+int fftconv_uniform_update_device(fftconv_uniform *h, const float *d_responses, size_t response_len,
+                                  size_t response_stride, void *hip_stream);
 /* FFTConvolver::reset, src/fft_convolver.rs:310-320 (all channels). */
 int fftconv_uniform_reset(fftconv_uniform *h);
 /* FFTConvolver::process, src/fft_convolver.rs:229-309, host buffers:
@@ -143,6 +148,9 @@ fftconv_crossfade *fftconv_crossfade_new(const fftconv_uniform *convolver, size_
 int fftconv_crossfade_update(fftconv_crossfade *h, const float *response, size_t response_len);
 int fftconv_crossfade_update_batch(fftconv_crossfade *h, const float *responses, size_t response_len,
                                    size_t response_stride);
+/* update() from device-resident responses, stream-ordered (see uniform). */
+int fftconv_crossfade_update_device(fftconv_crossfade *h, const float *d_responses, size_t response_len,
+                                    size_t response_stride, void *hip_stream);
 /* todo!() in the reference (src/crossfade_convolver.rs:80-82): FFTCONV_E_UNIMPLEMENTED. */
 int fftconv_crossfade_reset(fftconv_crossfade *h);
 /* src/crossfade_convolver.rs:66-78: input_len >= max_buffer_size and

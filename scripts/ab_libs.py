@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Same-process, interleaved A/B of several builds of libfftconv_amd.so on the
+cfg2 workload (methodology rule: never rank builds across processes/boxes).
+usage: ab_libs.py LIB1 LIB2 ... [--rounds R] [--steps K] [--channels C] [--block B] [--ir L]"""
+import argparse
+import ctypes as C
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fft-convolution_amd"))
+import numpy as np
+import torch
+
+from fftconv_amd import shard
+
+p = argparse.ArgumentParser()
+p.add_argument("libs", nargs="+")
+p.add_argument("--rounds", type=int, default=5)
+p.add_argument("--steps", type=int, default=200)
+p.add_argument("--channels", type=int, default=1024)
+p.add_argument("--block", type=int, default=256)
+p.add_argument("--ir", type=int, default=48000)
+a = p.parse_args()
+Cn, B, L = a.channels, a.block, a.ir
+torch.cuda.set_device(0)
+s = torch.cuda.Stream()
+torch.cuda.set_stream(s)
+irs = shard.synth_irs(range(Cn), L)
+x = torch.from_numpy(shard.synth_dry(range(Cn), 16, B)).cuda()
+handles = []
+for path in a.libs:
+    lib = C.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+    lib.fftconv_uniform_init_batch.restype = C.c_void_p
+    lib.fftconv_uniform_init_batch.argtypes = [C.c_int, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t]
+    lib.fftconv_uniform_process_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]
+    h = lib.fftconv_uniform_init_batch(0, Cn, irs.ctypes.data, L, L, B, L)
+    assert h, path
+    handles.append((lib, h, torch.empty((16, Cn, B), device="cuda")))
+res = [[] for _ in handles]
+k = 0
+for r in range(a.rounds):
+    for idx, (lib, h, y) in enumerate(handles):
+        for _ in range(20):
+            lib.fftconv_uniform_process_device(h, x[k % 16].data_ptr(), B, y[k % 16].data_ptr(), B, B, s.cuda_stream); k += 1
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(a.steps):
+            lib.fftconv_uniform_process_device(h, x[k % 16].data_ptr(), B, y[k % 16].data_ptr(), B, B, s.cuda_stream); k += 1
+        e1.record(s)
+        torch.cuda.synchronize()
+        res[idx].append(e0.elapsed_time(e1) * 1000 / a.steps)
+same = all(torch.equal(handles[0][2], hh[2]) for hh in handles[1:])
+for path, r in zip(a.libs, res):
+    us = statistics.median(r)
+    print(f"{path}: median {us:.2f} us/step (min {min(r):.2f}) -> {Cn * B / us:.1f} MS/s")
+print("outputs bit-identical across builds:", same)

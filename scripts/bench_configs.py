@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Throughput of the non-headline BASELINE.json configs on one GPU (HBM-resident
+inputs, HIP events on the launch stream).  Prints one JSON line per config.
+
+  cfg3: TwoStageFFTConvolver, head 64 / tail 4096, IR 262144, 256 channels,
+        one 64-sample process() per step.
+  cfg5: CrossfadeConvolver<FFTConvolver>, 512 channels, block 512, IR 96000,
+        update() with a fresh IR every 128 blocks (trait init: crossfade over
+        response.len() samples, so most updates take the pending path).
+
+Algorithmic bytes per output sample follow SURVEY.md §8(d)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fft-convolution_amd"))
+import numpy as np
+import torch
+
+import fftconv_amd as F
+from fftconv_amd import shard
+
+
+def uniform_bytes(B, L):
+    S = -(-L // B)
+    K = B + 1
+    return 16 * S * K + 8 * K + 16 * B  # per channel-block
+
+
+def run(conv, C, n_in, n_out, steps, warmup, ring, stream, update=None):
+    dev = torch.device("cuda:0")
+    xin = torch.from_numpy(shard.synth_dry(range(C), ring, n_in)).to(dev)
+    yout = torch.empty((ring, C, n_out), device=dev)
+    h = stream.cuda_stream
+    k = 0
+
+    def step(i):
+        r = i % ring
+        if update is not None:
+            update(i)
+        conv.process_device(xin[r].data_ptr(), n_in, yout[r].data_ptr(), n_out, n_out, h)
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(steps):
+        step(warmup + i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev = e0.elapsed_time(e1) / 1000
+    assert torch.isfinite(yout).all()
+    return max(wall, ev), ev
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--configs", default="3,5")
+    p.add_argument("--steps3", type=int, default=2048)
+    p.add_argument("--steps5", type=int, default=512)
+    a = p.parse_args()
+    torch.cuda.set_device(0)
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    out = []
+    if "3" in a.configs.split(","):
+        C, head, L = 256, 64, 262144
+        conv = F.TwoStageFFTConvolver.init(shard.synth_irs(range(C), L), head, L, channels=C)
+        T = conv.tail_block_size
+        t, ev = run(conv, C, head, head, a.steps3, 2 * T // head, 64, s)
+        samples = C * head * a.steps3
+        per_sample = (uniform_bytes(head, T) + uniform_bytes(head, T) + uniform_bytes(T, L - 2 * T) * head / T) / head
+        out.append({"config": "cfg3 TwoStageFFTConvolver", "channels": C, "head": head, "tail": T, "ir": L,
+                    "steps": a.steps3, "MSamples_s": round(samples / t / 1e6, 2),
+                    "us_per_step": round(t / a.steps3 * 1e6, 3),
+                    "algorithmic_GBs": round(samples * per_sample / ev / 1e9, 1),
+                    "bytes_per_sample": round(per_sample, 1)})
+        del conv
+    if "5" in a.configs.split(","):
+        C, B, L = 512, 512, 96000
+        irs = shard.synth_irs(range(C), L)
+        conv = F.CrossfadeConvolver.init(irs, B, L, channels=C)
+        # fresh IRs resident in HBM (like the inputs): update_device, stream-ordered
+        fresh = [torch.from_numpy(shard.synth_irs(range(1000 + 100 * j, 1000 + 100 * j + C), L)).cuda()
+                 for j in range(2)]
+        torch.cuda.synchronize()
+
+        def upd(i):
+            if i % 128 == 127:
+                conv.update_device(fresh[(i // 128) % 2].data_ptr(), L, L, s.cuda_stream)
+
+        t, ev = run(conv, C, B, B, a.steps5, 64, 16, s, update=upd)
+        samples = C * B * a.steps5
+        per_sample = 2 * uniform_bytes(B, L) / B
+        out.append({"config": "cfg5 CrossfadeConvolver, update every 128 blocks", "channels": C, "block": B,
+                    "ir": L, "steps": a.steps5, "MSamples_s": round(samples / t / 1e6, 2),
+                    "us_per_step": round(t / a.steps5 * 1e6, 3),
+                    "algorithmic_GBs_incl_updates": round(samples * per_sample / t / 1e9, 1),
+                    "bytes_per_sample": round(per_sample, 1),
+                    "note": "update_device() (HBM-resident IRs: S-segment FFTs per channel) is inside the timed region"})
+    for o in out:
+        print(json.dumps(o), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -271,6 +271,31 @@ def test_uniform_update_sequence(amd, oracle_mod):
         assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
 
 
+@pytest.mark.parametrize("kind", ["uniform", "crossfade"])
+def test_update_device_matches_host_update(amd, kind):
+    """update_device (HBM-resident responses, stream-ordered) == update (host)."""
+    import torch
+
+    rng = np.random.default_rng(60)
+    C, B, L = 4, 128, 1200
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    cls = amd.FFTConvolver if kind == "uniform" else amd.CrossfadeConvolver
+    a = cls.init(hs, B, L, channels=C)
+    b = cls.init(hs, B, L, channels=C)
+    s = torch.cuda.Stream()
+    for step in range(30):
+        if step in (5, 9, 17):
+            hn = np.stack([ir(rng, 900) for _ in range(C)])
+            a.update(hn)
+            d = torch.from_numpy(hn).cuda()
+            torch.cuda.synchronize()
+            b.update_device(d.data_ptr(), 900, 900, s.cuda_stream)
+            b.synchronize()
+            s.synchronize()
+        x = np.stack([white(rng, B) for _ in range(C)])
+        assert np.array_equal(a.process(x), b.process(x)), step
+
+
 def test_uniform_update_channel(amd, oracle_mod):
     rng = np.random.default_rng(12)
     C, B, L = 4, 128, 900
