@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -359,8 +360,39 @@ struct TwoStageCore {
 
     float *tail_input() const { return tin_buf[tin_idx].p; }
 
+    // The side stream is confined to the first ncu/k CUs (k =
+    // FFTCONV_TAIL_CU_DIV, default 3): a T-block tail workgroup fills a whole
+    // CU (1024 lanes x 128 VGPRs), and unconfined it locks the
+    // latency-critical head steps out of the chip for its whole duration
+    // (measured: a 197 us head step behind a 193 us tail).  Contiguous masks
+    // only: power-of-two strided masks read back fine but did not constrain
+    // dispatch (scripts/cumask_probe.hip).  k = 1 disables the mask.
+    int create_side_stream() {
+        // default share: the tail's fraction of the bytes streamed per tail
+        // period (cfg3: 4.06 MB of 12.5 MB per channel -> k = 3)
+        int k = 1;
+        if (tail) {
+            const double tail_b = (double)tail->S * (double)tail->B;
+            double per_b = tail_b + (double)(T / std::max<size_t>(head_bs, 1)) *
+                                        (double)((head ? head->S * head->B : 0) + (tail0 ? tail0->S * tail0->B : 0));
+            k = (int)std::lround(per_b / std::max(tail_b, 1.0));
+            k = std::min(8, std::max(2, k));
+        }
+        if (const char *e = getenv("FFTCONV_TAIL_CU_DIV")) k = std::max(1, atoi(e));
+        int ncu = 0;
+        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        if (k <= 1 || ncu <= 0) {
+            HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+            return FFTCONV_OK;
+        }
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int cu = 0; cu < std::max(1, ncu / k); ++cu) mask[cu / 32] |= 1u << (cu % 32);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
+        return FFTCONV_OK;
+    }
+
     int alloc_buffers() {
-        HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        if (int r = create_side_stream()) return r;
         HIP_TRY(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming));
         for (auto *b : {&out0, &pre0, &out1, &pre1, &tin_buf[0], &tin_buf[1]}) {
@@ -903,6 +935,18 @@ int fftconv_uniform_process_device(fftconv_uniform *h, const float *d_input, siz
     DeviceGuard g(h->core.device);
     return h->core.process_device(d_input, in_stride, d_output, out_stride, len, pick(hip_stream, h->core.stream));
 }
+int fftconv_uniform_process_device_steps(fftconv_uniform *h, const float *d_input, size_t in_stride, size_t in_step,
+                                   float *d_output, size_t out_stride, size_t out_step, size_t len, size_t steps,
+                                   void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    for (size_t k = 0; k < steps; ++k) {
+        if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
+            return r;
+    }
+    return FFTCONV_OK;
+}
 fftconv_uniform *fftconv_uniform_clone(const fftconv_uniform *h) {
     if (!h) { set_error("null handle"); return nullptr; }
     auto *c = new (std::nothrow) fftconv_uniform();
@@ -957,6 +1001,18 @@ int fftconv_twostage_process_device(fftconv_twostage *h, const float *d_input, s
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
     return h->core.process_device(d_input, in_stride, d_output, out_stride, len, pick(hip_stream, h->core.stream));
+}
+int fftconv_twostage_process_device_steps(fftconv_twostage *h, const float *d_input, size_t in_stride, size_t in_step,
+                                   float *d_output, size_t out_stride, size_t out_step, size_t len, size_t steps,
+                                   void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    for (size_t k = 0; k < steps; ++k) {
+        if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
+            return r;
+    }
+    return FFTCONV_OK;
 }
 fftconv_twostage *fftconv_twostage_clone(const fftconv_twostage *h) {
     if (!h) { set_error("null handle"); return nullptr; }
@@ -1030,6 +1086,18 @@ int fftconv_crossfade_process_device(fftconv_crossfade *h, const float *d_input,
                                   pick(hip_stream, h->core.stream));
 }
 int fftconv_crossfade_is_crossfading(const fftconv_crossfade *h) { return h && h->core.is_crossfading() ? 1 : 0; }
+int fftconv_crossfade_process_device_steps(fftconv_crossfade *h, const float *d_input, size_t in_stride, size_t in_step,
+                                   float *d_output, size_t out_stride, size_t out_step, size_t len, size_t steps,
+                                   void *hip_stream) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    DeviceGuard g(h->core.device);
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    for (size_t k = 0; k < steps; ++k) {
+        if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
+            return r;
+    }
+    return FFTCONV_OK;
+}
 fftconv_crossfade *fftconv_crossfade_clone(const fftconv_crossfade *h) {
     if (!h) { set_error("null handle"); return nullptr; }
     auto *c = new (std::nothrow) fftconv_crossfade();

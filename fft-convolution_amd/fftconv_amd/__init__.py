@@ -52,6 +52,7 @@ SIGNATURES = {
     "fftconv_uniform_reset": (_i, [_vp]),
     "fftconv_uniform_process": (_i, [_vp, _fp, _sz, _fp, _sz]),
     "fftconv_uniform_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
+    "fftconv_uniform_process_device_steps": (_i, [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _sz, _sz, _vp]),
     "fftconv_uniform_clone": (_vp, [_vp]),
     "fftconv_uniform_destroy": (None, [_vp]),
     "fftconv_uniform_synchronize": (_i, [_vp]),
@@ -65,6 +66,7 @@ SIGNATURES = {
     "fftconv_twostage_reset": (_i, [_vp]),
     "fftconv_twostage_process": (_i, [_vp, _fp, _fp, _sz]),
     "fftconv_twostage_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
+    "fftconv_twostage_process_device_steps": (_i, [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _sz, _sz, _vp]),
     "fftconv_twostage_clone": (_vp, [_vp]),
     "fftconv_twostage_destroy": (None, [_vp]),
     "fftconv_twostage_synchronize": (_i, [_vp]),
@@ -78,6 +80,7 @@ SIGNATURES = {
     "fftconv_crossfade_reset": (_i, [_vp]),
     "fftconv_crossfade_process": (_i, [_vp, _fp, _sz, _fp, _sz]),
     "fftconv_crossfade_process_device": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _vp]),
+    "fftconv_crossfade_process_device_steps": (_i, [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _sz, _sz, _vp]),
     "fftconv_crossfade_is_crossfading": (_i, [_vp]),
     "fftconv_crossfade_clone": (_vp, [_vp]),
     "fftconv_crossfade_destroy": (None, [_vp]),
@@ -218,6 +221,13 @@ class _Base:
     def process_device(self, d_in: int, in_stride: int, d_out: int, out_stride: int, n: int, stream: int = 0):
         _check(self._fn("process_device")(self._h, C.c_void_p(d_in), in_stride, C.c_void_p(d_out), out_stride, n,
                                           C.c_void_p(stream) if stream else None))
+
+    def process_device_steps(self, d_in: int, in_stride: int, in_step: int, d_out: int, out_stride: int,
+                             out_step: int, n: int, steps: int, stream: int = 0):
+        """`steps` consecutive process_device calls (offsets in floats)."""
+        _check(self._fn("process_device_steps")(self._h, C.c_void_p(d_in), in_stride, in_step, C.c_void_p(d_out),
+                                                out_stride, out_step, n, steps,
+                                                C.c_void_p(stream) if stream else None))
 
     def __copy__(self):
         return self.clone()

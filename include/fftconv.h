@@ -103,6 +103,13 @@ int fftconv_uniform_process(fftconv_uniform *h, const float *input, size_t input
  * + len] and writes d_output[c*out_stride .. + len]. */
 int fftconv_uniform_process_device(fftconv_uniform *h, const float *d_input, size_t in_stride,
                                    float *d_output, size_t out_stride, size_t len, void *hip_stream);
+/* `steps` consecutive process() calls of `len` samples each, from one host
+ * call: call k reads d_input + k*in_step (channel stride in_stride) and writes
+ * d_output + k*out_step.  Identical to `steps` calls of _process_device; it
+ * removes the per-call host overhead when blocks are already resident. */
+int fftconv_uniform_process_device_steps(fftconv_uniform *h, const float *d_input, size_t in_stride,
+                                         size_t in_step, float *d_output, size_t out_stride,
+                                         size_t out_step, size_t len, size_t steps, void *hip_stream);
 /* #[derive(Clone)]: a deep, device-side copy of every buffer and scalar. */
 fftconv_uniform *fftconv_uniform_clone(const fftconv_uniform *h);
 void fftconv_uniform_destroy(fftconv_uniform *h);
@@ -127,6 +134,9 @@ int fftconv_twostage_reset(fftconv_twostage *h);
 int fftconv_twostage_process(fftconv_twostage *h, const float *input, float *output, size_t len);
 int fftconv_twostage_process_device(fftconv_twostage *h, const float *d_input, size_t in_stride,
                                     float *d_output, size_t out_stride, size_t len, void *hip_stream);
+int fftconv_twostage_process_device_steps(fftconv_twostage *h, const float *d_input, size_t in_stride,
+                                          size_t in_step, float *d_output, size_t out_stride,
+                                          size_t out_step, size_t len, size_t steps, void *hip_stream);
 fftconv_twostage *fftconv_twostage_clone(const fftconv_twostage *h);
 void fftconv_twostage_destroy(fftconv_twostage *h);
 int fftconv_twostage_synchronize(fftconv_twostage *h);
@@ -160,6 +170,10 @@ int fftconv_crossfade_process(fftconv_crossfade *h, const float *input, size_t i
 int fftconv_crossfade_process_device(fftconv_crossfade *h, const float *d_input, size_t in_stride,
                                      float *d_output, size_t out_stride, size_t output_len,
                                      void *hip_stream);
+int fftconv_crossfade_process_device_steps(fftconv_crossfade *h, const float *d_input, size_t in_stride,
+                                           size_t in_step, float *d_output, size_t out_stride,
+                                           size_t out_step, size_t output_len, size_t steps,
+                                           void *hip_stream);
 int fftconv_crossfade_is_crossfading(const fftconv_crossfade *h); /* :85-92, 1/0 */
 fftconv_crossfade *fftconv_crossfade_clone(const fftconv_crossfade *h);
 void fftconv_crossfade_destroy(fftconv_crossfade *h);

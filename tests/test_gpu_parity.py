@@ -296,6 +296,27 @@ def test_update_device_matches_host_update(amd, kind):
         assert np.array_equal(a.process(x), b.process(x)), step
 
 
+@pytest.mark.parametrize("kind", ["uniform", "twostage", "crossfade"])
+def test_process_device_steps_equals_calls(amd, kind):
+    """process_device_steps(K) is bit-identical to K process_device calls."""
+    import torch
+
+    rng = np.random.default_rng(70)
+    C, B, L, K = 3, 64, 3000, 40
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    cls = {"uniform": amd.FFTConvolver, "twostage": amd.TwoStageFFTConvolver,
+           "crossfade": amd.CrossfadeConvolver}[kind]
+    a, b = cls.init(hs, B, L, channels=C), cls.init(hs, B, L, channels=C)
+    x = torch.from_numpy(np.stack([np.stack([white(rng, B) for _ in range(C)]) for _ in range(K)])).cuda()
+    ya, yb = torch.zeros_like(x), torch.zeros_like(x)
+    s = torch.cuda.Stream()
+    for k in range(K):
+        a.process_device(x[k].data_ptr(), B, ya[k].data_ptr(), B, B, s.cuda_stream)
+    b.process_device_steps(x.data_ptr(), B, C * B, yb.data_ptr(), B, C * B, B, K, s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(ya, yb)
+
+
 def test_uniform_update_channel(amd, oracle_mod):
     rng = np.random.default_rng(12)
     C, B, L = 4, 128, 900
