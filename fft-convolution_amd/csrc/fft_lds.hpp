@@ -42,11 +42,28 @@ __device__ __forceinline__ float2 twmul(float2 a, float2 w) { return INV ? cmulc
 template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) { return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x); }
 
+// Wave-local LDS ordering point: one wave's LDS writes are visible to all its
+// lanes' later reads (DS ops of a wave execute in order; the wait and the
+// compiler barrier keep the reads behind the writes).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool WAVE>
+__device__ __forceinline__ void stage_sync() {
+    if constexpr (WAVE) wave_sync();
+    else __syncthreads();
+}
+
 // M-point complex FFT (M = 2^LOG2M) over LDS, executed by NT threads.
 // Input in buf0; returns the buffer that holds the naturally ordered result
 // (buf0 or buf1).  INV = unnormalised inverse (conjugate twiddles).
-// `tw` is the W_N table with N = 2M.  Every thread of the block must call it.
-template <int LOG2M, int NT, bool INV>
+// `tw` is the W_N table with N = 2M.  Every thread of the block must call it
+// (WAVE: a single wave -- NT = 64 -- calls it, synchronising at wave level).
+template <int LOG2M, int NT, bool INV, bool WAVE = false>
 __device__ __forceinline__ float2 *lds_cfft(float2 *buf0, float2 *buf1, const float2 *__restrict__ tw) {
     constexpr int M = 1 << LOG2M;
     constexpr int N = 2 * M;
@@ -77,7 +94,7 @@ __device__ __forceinline__ float2 *lds_cfft(float2 *buf0, float2 *buf1, const fl
             dst[base + 2 * Ns] = csub(a02, a13);
             dst[base + 3 * Ns] = csub(s02, s13);
         }
-        __syncthreads();
+        stage_sync<WAVE>();
         float2 *t = src; src = dst; dst = t;
     }
     if constexpr ((LOG2M & 1) != 0) {
@@ -92,7 +109,7 @@ __device__ __forceinline__ float2 *lds_cfft(float2 *buf0, float2 *buf1, const fl
             dst[base] = cadd(v0, v1);
             dst[base + Ns] = csub(v0, v1);
         }
-        __syncthreads();
+        stage_sync<WAVE>();
         float2 *t = src; src = dst; dst = t;
     }
     return src;

@@ -769,8 +769,17 @@ struct CrossfadeCore {
             response_pending = false;
         }
         const size_t m = max_buffer_size;
-        if (int r = a->process_device(din, is, buf_a.p, m, m, s)) return r;   // :72
-        if (int r = b->process_device(din, is, buf_b.p, m, m, s)) return r;   // :73
+        if (m > (size_t)INT32_MAX) return fail(FFTCONV_E_UNSUPPORTED, "process length exceeds 2^31-1");
+        if (m > 0 && C > 0) {
+            // :72-73 -- A and B are two jobs of ONE launch (same block size):
+            // 2C workgroups fill the chip where C alone leaves it half occupied
+            ProcArgs pa{};
+            pa.job[0] = a->job(din, is, buf_a.p, m, m);
+            pa.job[1] = b->job(din, is, buf_b.p, m, m);
+            pa.njobs = 2;
+            pa.tw = a->tw.p;
+            HIP_TRY(launch_process(a->log2b, pa, (int)C, s));
+        }
         CrossfadeMixArgs x{};
         x.buf_a = buf_a.p; x.buf_b = buf_b.p; x.buf_stride = (long long)m;
         x.out = dout; x.out_stride = (long long)os; x.n = (int)out_len;
@@ -873,11 +882,16 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 3) return fail(FFTCONV_E_INVALID, "variant must be 0..3 (or -1 = auto)");
+    if (variant > 7) return fail(FFTCONV_E_INVALID, "variant must be 0..7 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }
 int fftconv_get_kernel_variant(void) { return get_variant(); }
+int fftconv_set_pipeline_lag(int rows) {
+    set_pipeline_lag(rows);
+    return FFTCONV_OK;
+}
+int fftconv_get_pipeline_lag(void) { return get_pipeline_lag(); }
 
 // ---- uniform --------------------------------------------------------------
 fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len, size_t max_block_size,

@@ -16,6 +16,8 @@
 // loads (float4 = 2 bins per lane).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 #include <type_traits>
 
 #include "fft_lds.hpp"
@@ -40,7 +42,13 @@ struct Geo {
     static constexpr bool PREFETCH = LOG2B <= 9;
     static constexpr size_t tw_bytes = PREFETCH ? 2 * (size_t)B * sizeof(float2) : 0;
     static constexpr size_t pre_bytes = PREFETCH ? (size_t)B * sizeof(float2) + 3 * (size_t)B * sizeof(float) : 0;
-    static constexpr size_t lds_bytes = ((2 * (size_t)B * sizeof(float2) + red_bytes + tw_bytes + pre_bytes + 15) / 16) * 16 + 16;
+    static constexpr size_t gen_bytes = ((2 * (size_t)B * sizeof(float2) + red_bytes + tw_bytes + pre_bytes + 15) / 16) * 16;
+    // pipelined full-block step (pipelined_step): bufA | bufB | tw (2B) | H0 | H1 | pre | overlap | tail0 | tail1
+    static constexpr bool PIPE = LOG2B >= 1 && LOG2B <= 9 && NT == 256;
+    // (the closing reduction reuses the front: 4 waves x 64 lanes x 16 B x slots/lane)
+    static constexpr size_t pipe_red = 4 * 64 * 16 * (size_t)(B >= 128 ? B / 128 : 1);
+    static constexpr size_t pipe_bytes = PIPE ? (68 * (size_t)B > pipe_red ? 68 * (size_t)B : pipe_red) : 0;
+    static constexpr size_t lds_bytes = (gen_bytes > pipe_bytes ? gen_bytes : pipe_bytes) + 16;
 };
 
 template <int VEC> struct VecT;
@@ -234,6 +242,215 @@ __device__ __forceinline__ void twostage_epilogue(const ProcJob &J, size_t c, fl
     }
 }
 
+// FDL stream of the pipelined step: rows i = 2 + t of the NEXT block's
+// pre_multiplied (block start `curp`) for t in [t_begin, t_end), split over
+// nw waves (this is wave sw of them); a wave covers RPW rows at once when a
+// row has fewer than 64 slots.  Accumulates into acc (not zeroed here).
+template <int LOG2B, bool NTL, class AccArr>
+__device__ __forceinline__ void mac_rows_range(AccArr &acc, const float2 *Hc, const float2 *Xc, int S, int curp,
+                                               int act, int t_begin, int t_end, int nw, int sw, int rsub, int f0) {
+    constexpr int B = 1 << LOG2B, F = B / 2;
+    constexpr int RPW = F >= 64 ? 1 : 64 / F, SPL = F >= 64 ? F / 64 : 1;
+    constexpr int U = SPL == 1 ? 8 : (SPL == 2 ? 4 : 2);
+    constexpr int ROWB = B * (int)sizeof(float2);
+    constexpr bool UNIFORM = RPW == 1;  // one row per wave-iteration: row offset in an SGPR
+    const int STEP = nw * RPW;
+    const size_t bytes = (size_t)S * ROWB;
+    const RowStream hs(Hc, bytes), xs(Xc, bytes);
+    const int lane_off = f0 * 16;
+    int t = t_begin + sw * RPW + rsub;
+    int i = 2 + t;
+    int xi = (curp + i) % act;
+    for (; t + (U - 1) * STEP < t_end; t += U * STEP) {
+        float4 hv[U][SPL], xv[U][SPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ho = i * ROWB, xo = xi * ROWB;
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) {
+                const int lo = lane_off + s * 64 * 16;
+                hv[u][s] = UNIFORM ? hs.ld4<NTL>(lo, ho) : hs.ld4<NTL>(lo + ho, 0);
+                xv[u][s] = UNIFORM ? xs.ld4<NTL>(lo, xo) : xs.ld4<NTL>(lo + xo, 0);
+            }
+            i += STEP;
+            xi += STEP;
+            if (xi >= act) xi -= act;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) acc[s].mac(hv[u][s], xv[u][s]);
+    }
+    for (; t < t_end; t += STEP) {
+        const int ho = i * ROWB, xo = xi * ROWB;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            const int lo = lane_off + s * 64 * 16;
+            const float4 h = UNIFORM ? hs.ld4<NTL>(lo, ho) : hs.ld4<NTL>(lo + ho, 0);
+            const float4 x = UNIFORM ? xs.ld4<NTL>(lo, xo) : xs.ld4<NTL>(lo + xo, 0);
+            acc[s].mac(h, x);
+        }
+        i += STEP;
+        xi += STEP;
+        if (xi >= act) xi -= act;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined full-block step (2 <= B <= 512): the common call -- one whole
+// block from an empty input buffer -- when pre[] already holds
+// pre_multiplied for the block at `current` (FLAG_PRE).  The work of
+// FFTConvolver::process (:229-309) is re-timed, not changed:
+//   wave 0   : R2C of the block -> FDL row `current`; conv = pre + X.H[0];
+//              C2R, x1/N; overlap-add and overlap save -- all out of LDS,
+//              staged by its own LDS-DMA, synchronised at wave level; then
+//              row 1 (H[1] (.) X_new) of the NEXT block's pre_multiplied,
+//              then the last w0 = max(0, (S-2-lag)/4) FDL rows of it
+//   waves 1-3: stream the other FDL rows of the NEXT block's pre_multiplied
+// so the latency chain hides under the FDL stream instead of following it
+// (lag ~ the chain's duration in rows of stream; set by the host).
+// The next block's pre is reduced in a fixed order and stored (FLAG_PRE).
+// ---------------------------------------------------------------------------
+template <int LOG2B, int NT, bool NTL>
+__device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob &J, size_t c, int cur, int act,
+                                               int flags, unsigned char *smem) {
+    using Gm = Geo<LOG2B, NT>;
+    constexpr int B = Gm::B, F = B / 2;
+    constexpr int RPW = F >= 64 ? 1 : 64 / F, SPL = F >= 64 ? F / 64 : 1;
+    constexpr int NSW = NT / 64 - 1;
+    constexpr float invN = 1.0f / (float)(2 * B);
+    float2 *bufA = reinterpret_cast<float2 *>(smem);
+    float2 *bufB = bufA + B;
+    float2 *twl = bufB + B;
+    float2 *h0l = twl + 2 * B;
+    float2 *h1l = h0l + B;
+    float2 *prel = h1l + B;
+    float *ovl = reinterpret_cast<float *>(prel + B);
+    float *p0l = ovl + B;
+    float *p1l = p0l + B;
+    int &s_err = *reinterpret_cast<int *>(smem + Gm::lds_bytes - 16);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const size_t rows = (size_t)J.S * B;
+    const float2 *Hc = J.H + c * rows;
+    float2 *Xc = J.X + c * rows;
+    float *ovc = J.overlap + c * B;
+    float2 *prec = J.pre + c * B;
+    float *outc = J.out + c * J.out_stride;
+    const float *inc = J.in + c * J.in_stride;
+    const int curp = cur > 0 ? cur - 1 : act - 1;  // current after this block (:301-305)
+    const int rsub = F >= 64 ? 0 : lane / F;
+    const int f0 = F >= 64 ? lane : lane % F;
+
+    Acc2 acc[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) acc[s].zero();
+    if (wave == 0) {
+        // ---- critical chain, one wave ----
+        dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);   // x[0..B) as packed z[0..B/2)
+        for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
+        dma_16b<64>(twl, a.tw, 2 * B * (int)sizeof(float2));
+        dma_16b<64>(h0l, Hc, B * (int)sizeof(float2));
+        if (act > 1) dma_16b<64>(h1l, Hc + B, B * (int)sizeof(float2));
+        dma_16b<64>(prel, prec, B * (int)sizeof(float2));
+        dma_f32<64>(ovl, ovc, B);
+        if (J.add0) dma_f32<64>(p0l, J.add0 + c * J.add_stride, B);
+        if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_sync();
+        if (J.tin) {  // two-stage: append the block to tail_input (:473-475)
+            const float *xb = reinterpret_cast<const float *>(bufA);
+            float *ti = J.tin + c * J.tin_stride;
+            for (int j = lane; j < B; j += 64) ti[j] = xb[j];
+        }
+        wave_sync();
+        float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :243-255
+        float2 *Q = Z == bufA ? bufB : bufA;
+        float2 *Xcur = Xc + (size_t)cur * B;
+        for (int m = lane; m < B; m += 64) {
+            const float2 v = real_post<LOG2B, 64>(Z, m, twl);
+            Q[m] = v;
+            Xcur[m] = v;
+        }
+        wave_sync();
+        bool bad = false;  // conv = pre + X (.) H[0] (:270-275), then the C2R error check
+        for (int f = lane; f < F; f += 64) {
+            const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
+                                       reinterpret_cast<const float4 *>(h0l)[f], f);
+            reinterpret_cast<float4 *>(Z)[f] = cv;
+            if (f == 0 && !slot0_finite(cv)) bad = true;
+        }
+        // row 1 of the next block's pre_multiplied: H[1] (.) X_new (X_new is row (curp+1) % act = cur)
+        if (act > 1 && rsub == 0) {
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) {
+                const int f = f0 + s * 64;
+                if (f < F) acc[s].mac(reinterpret_cast<const float4 *>(h1l)[f], reinterpret_cast<const float4 *>(Q)[f]);
+            }
+        }
+        const bool err = __ballot(bad) != 0ull;
+        wave_sync();
+        if (!err) {
+            for (int m = lane; m < B; m += 64) Q[m] = real_pre<LOG2B, 64>(Z, m, twl);
+            wave_sync();
+            const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(Q, Z, twl));
+            for (int j = lane; j < B; j += 64) {  // overlap-add (:284-288) + two-stage adds (:453-468)
+                float v = y[j] * invN + ovl[j];
+                if (J.add0) {
+                    v += p0l[j];
+                    if (J.add1) v += p1l[j];
+                }
+                outc[j] = v;
+                ovc[j] = y[B + j] * invN;  // :297-298
+            }
+        } else {
+            // output.fill(0); return (:278-281): the block stays in the input
+            // buffer, fill / current unchanged, pre still describes this block
+            float *ibc = J.inbuf + c * B;
+            for (int j = lane; j < B; j += 64) {
+                float v = 0.f;
+                if (J.add0) {
+                    v += p0l[j];
+                    if (J.add1) v += p1l[j];
+                }
+                outc[j] = v;
+                ibc[j] = inc[j];
+            }
+        }
+        if (lane == 0) s_err = err ? 1 : 0;
+    }
+    // ---- FDL rows 2..act-1 of the next block's pre: waves 1..NSW take
+    // t in [0, R0), wave 0 (after its chain) the last w0 rows ----
+    {
+        const int R = act > 2 ? act - 2 : 0;
+        const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
+        const int R0 = R - w0;
+        if (wave == 0) mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, R0, R, 1, 0, rsub, f0);
+        else mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R0, NSW, wave - 1, rsub, f0);
+    }
+    __syncthreads();
+    if (s_err) {
+        if (tid == 0) J.state[c] = make_int4(cur, act, 0, flags | FLAG_INBUF);
+        return;
+    }
+    // next block's pre: every lane parks its partial sums in LDS (the whole
+    // workgroup's staging is dead now), then slot f sums waves 0..NSW and
+    // sub-rows in a fixed order -- deterministic for a given geometry and lag
+    float4 *red = reinterpret_cast<float4 *>(smem);
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) red[(wave * SPL + s) * 64 + lane] = acc[s].get(f0 + s * 64);
+    __syncthreads();
+    for (int f = tid; f < F; f += NT) {
+        const int base = (f / 64) * 64 + f % 64;
+        float4 p = red[base];
+        for (int w = 0; w <= NSW; ++w)
+            for (int r = (w == 0 ? 1 : 0); r < RPW; ++r) p = vadd(p, red[w * SPL * 64 + base + r * F]);
+        reinterpret_cast<float4 *>(prec)[f] = p;
+    }
+    if (tid == 0) J.state[c] = make_int4(curp, act, 0, ((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE);
+}
+
 // ---------------------------------------------------------------------------
 // Fused UPOLS step: FFTConvolver::process (src/fft_convolver.rs:229-309) for
 // one channel per workgroup, the whole chunk loop of one call on device.
@@ -273,6 +490,13 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
         for (int j = tid; j < n; j += NT) outc[j] = 0.f;
         twostage_epilogue<NT>(J, c, outc, inc, n);
         return;
+    }
+
+    if constexpr (Gm::PIPE) {
+        if (a.pipe && fill == 0 && n == B && !(flags & FLAG_INBUF) && (flags & FLAG_PRE) && cur < act && !ZZ) {
+            pipelined_step<LOG2B, NT, NTL>(a, J, c, cur, act, flags, smem);
+            return;
+        }
     }
 
     const size_t rows = (size_t)J.S * B;
@@ -328,12 +552,26 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
     }
 
     int processed = 0;
-    bool err = false;
-    while (processed < n) {
+    bool err = false, pre_next = false;
+    for (;;) {
         const bool was_empty = fill == 0;                               // :237
         const int k = min(n - processed, B - fill);                      // :238-241
+        if (processed >= n) {
+            // a full-block call that ended on a block boundary: one more MAC
+            // pass (no transform) computes the next block's pre_multiplied so
+            // the following full-block call takes pipelined_step
+            if (!Gm::PIPE || ZZ || !a.pipe || n != B || !was_empty || (flags & FLAG_PRE) || cur >= act) break;
+            pre_next = true;
+        }
 
-        if (was_empty) {                                                 // :258-269
+        if (was_empty && (flags & FLAG_PRE) && cur < act) {
+            // pre[] already holds this block's pre_multiplied (computed at the
+            // end of the previous block)
+            if (owner) {
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) pacc[s] = reinterpret_cast<const vec_t *>(prec)[f0 + s * NT];
+            }
+        } else if (was_empty) {                                          // :258-269
             AccT<VEC> acc[SPT];
             mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, J.S, cur, act, flags, f0, g);
             if constexpr (G > 1) {
@@ -349,6 +587,10 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
 #pragma unroll
                 for (int s = 0; s < SPT; ++s) pacc[s] = acc[s].get(f0 + s * NT);
             }
+        }
+        if (pre_next) {
+            flags |= FLAG_PRE;
+            break;
         }
 
         // forward FFT of the zero-padded input buffer into segments[current]
@@ -431,7 +673,7 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
             for (int j = tid; j < B; j += NT) ovc[j] = y[B + j] * invN;  // :297-298
             if (flags & FLAG_INBUF)
                 for (int j = tid; j < B; j += NT) ibc[j] = 0.f;           // :294
-            flags &= ~FLAG_INBUF;
+            flags &= ~(FLAG_INBUF | FLAG_PRE);
             flags ^= FLAG_REV;
             fill = 0;
             cur = cur > 0 ? cur - 1 : act - 1;                            // :301-305
@@ -452,7 +694,7 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
         flags |= FLAG_INBUF;
         for (int j = tid; j < n; j += NT) outc[j] = 0.f;
     }
-    if ((fill != 0 || err) && owner) {
+    if ((fill != 0 || err || pre_next) && owner) {
 #pragma unroll
         for (int s = 0; s < SPT; ++s) reinterpret_cast<vec_t *>(prec)[f0 + s * NT] = pacc[s];
     }
@@ -484,7 +726,10 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
             a.overlap[c * B + j] = 0.f;
             a.pre[c * B + j] = make_float2(0.f, 0.f);
         }
-        if (tid == 0) a.state[c].y = (int)active;
+        if (tid == 0) {
+            a.state[c].y = (int)active;
+            a.state[c].w &= ~FLAG_PRE;  // the stored pre used the old response
+        }
     }
     if (i >= active) {  // :224-226
         for (int j = tid; j < B; j += NT) row[j] = make_float2(0.f, 0.f);
@@ -583,6 +828,15 @@ constexpr int kNT = 256;
 constexpr int proc_nt(int log2b) { return log2b <= 10 ? 256 : (log2b == 11 ? 512 : 1024); }
 
 static int g_variant = VARIANT_AUTO;
+static int g_lag = -1;
+
+// Pipelined step: FDL rows the three stream waves take alone while wave 0
+// runs the transform chain.  Auto: all of them -- wave 0 never streams (cfg3
+// head, S = 64, swept in-process: lag 0 1527, 16 1586, 32 1635, 48 1754,
+// >= 62 1844 MS/s; the chain is the critical path, any row given to wave 0
+// lengthens it).  Never a function of the channel count, so channel shards
+// of any size stay bit-identical.
+static int pipeline_lag(int) { return g_lag >= 0 ? g_lag : (1 << 30); }
 
 // Automatic variant: a per-step H+X stream larger than the 256 MiB Infinity
 // Cache is re-read from HBM every step whatever the load policy, and there
@@ -592,11 +846,23 @@ static int g_variant = VARIANT_AUTO;
 // so the choice never changes a result bit; zig-zag (+0.6 % on top of NT)
 // changes the summation order and is therefore opt-in only, keeping channel
 // shards bit-identical whatever the shard size.
+//
+// The pipelined full-block step pays off where a channel's FDL stream is
+// short next to its transform chain (cfg3's head, S*B = 4096: 1630 -> 1860
+// MS/s) and costs ~3 % on long ones (cfg2, S*B = 48128: the other resident
+// workgroups' streams already cover each chain, and three stream waves issue
+// fewer loads than four).  It changes the summation order, so it is chosen
+// per channel geometry (never by channel count): shards stay bit-identical.
 static int pick_variant(const ProcArgs &a, int channels, int log2b) {
     if (g_variant != VARIANT_AUTO) return g_variant;
     double stream = 0.0;
-    for (int j = 0; j < a.njobs; ++j) stream += 16.0 * (double)channels * (double)a.job[j].S * (double)(1 << log2b);
-    return stream > 192.0 * 1024 * 1024 ? VARIANT_NT : 0;
+    long long rows = 0;
+    for (int j = 0; j < a.njobs; ++j) {
+        stream += 16.0 * (double)channels * (double)a.job[j].S * (double)(1 << log2b);
+        rows = std::max(rows, (long long)a.job[j].S);
+    }
+    const int nt = stream > 192.0 * 1024 * 1024 ? VARIANT_NT : 0;
+    return nt | ((rows << log2b) > 16384 ? VARIANT_NOPIPE : 0);
 }
 
 template <int LOG2B>
@@ -604,7 +870,11 @@ static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t 
     constexpr int PNT = proc_nt(LOG2B);
     using Gm = Geo<LOG2B, PNT>;
     auto kern = upols_process_kernel<LOG2B, PNT, false, false>;
-    switch (pick_variant(a, channels, LOG2B) & 3) {
+    const int var = pick_variant(a, channels, LOG2B);
+    ProcArgs args = a;
+    args.pipe = (var & VARIANT_NOPIPE) ? 0 : 1;
+    args.lag = pipeline_lag(LOG2B);
+    switch (var & 3) {
         case 1: kern = upols_process_kernel<LOG2B, PNT, true, false>; break;
         case 2: kern = upols_process_kernel<LOG2B, PNT, false, true>; break;
         case 3: kern = upols_process_kernel<LOG2B, PNT, true, true>; break;
@@ -615,7 +885,7 @@ static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t 
                                            (int)Gm::lds_bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(channels, a.njobs), dim3(PNT), Gm::lds_bytes, s, a);
+    hipLaunchKernelGGL(kern, dim3(channels, a.njobs), dim3(PNT), Gm::lds_bytes, s, args);
     return hipGetLastError();
 }
 
@@ -672,7 +942,9 @@ hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStre
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 3); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 7); }
+void set_pipeline_lag(int rows) { g_lag = rows < 0 ? -1 : rows; }
+int get_pipeline_lag() { return g_lag; }
 int get_variant() { return g_variant == VARIANT_AUTO ? -1 : g_variant; }
 
 hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s) {

@@ -8,12 +8,15 @@ namespace fftconv {
 enum : int {
     FLAG_INBUF = 1,  // the HBM input buffer holds live samples
     FLAG_REV = 2,    // scan parity of the segment MAC (toggled per completed block)
+    FLAG_PRE = 4,    // pre[] holds pre_multiplied of the block that starts at `current`
 };
 
 // fused-kernel variants (bit mask): 1 = zig-zag segment scan, 2 = nontemporal H/X loads
-enum : int { VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_AUTO = 0x7fffffff };
+enum : int { VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_NOPIPE = 4, VARIANT_AUTO = 0x7fffffff };
 void set_variant(int v);
 int get_variant();
+void set_pipeline_lag(int rows);
+int get_pipeline_lag();
 
 // One convolver batch's call (FFTConvolver::process over `n` samples of every
 // channel), optionally with the two-stage epilogue of the head block
@@ -45,6 +48,8 @@ struct ProcArgs {
     ProcJob job[2];
     const float2 *tw;      // W_N^k, k < N = 2B
     int njobs;
+    int pipe;              // pipelined full-block step allowed (B <= 512)
+    int lag;               // pipelined step: FDL rows wave 0 leaves to the stream waves
 };
 
 struct IrArgs {

@@ -24,7 +24,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libfftconv_amd.so")
+# FFTCONV_AMD_LIB: another build of the same library (A/B of kernel revisions)
+LIB_PATH = os.environ.get("FFTCONV_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "libfftconv_amd.so")
 
 FFTCONV_OK = 0
 FFTCONV_E_INVALID = -1
@@ -43,6 +44,8 @@ SIGNATURES = {
     "fftconv_compute_tail_block_size": (_sz, [_sz, _sz]),
     "fftconv_set_kernel_variant": (_i, [_i]),
     "fftconv_get_kernel_variant": (_i, []),
+    "fftconv_set_pipeline_lag": (_i, [_i]),
+    "fftconv_get_pipeline_lag": (_i, []),
     "fftconv_uniform_init": (_vp, [_fp, _sz, _sz, _sz]),
     "fftconv_uniform_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
     "fftconv_uniform_update": (_i, [_vp, _fp, _sz]),
@@ -176,6 +179,15 @@ def set_kernel_variant(v: int):
 
 def get_kernel_variant() -> int:
     return int(lib().fftconv_get_kernel_variant())
+
+
+def set_pipeline_lag(rows: int):
+    """FDL rows the pipelined step leaves to its stream waves (-1 = automatic)."""
+    _check(lib().fftconv_set_pipeline_lag(rows))
+
+
+def get_pipeline_lag() -> int:
+    return int(lib().fftconv_get_pipeline_lag())
 
 
 def device_count() -> int:

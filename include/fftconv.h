@@ -60,12 +60,22 @@ size_t fftconv_complex_size(size_t size);         /* src/fft_convolver.rs:66-68 
 size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /* :534-540 */
 /* Tuning knob (process-wide): spectral-MAC scan variant of the fused kernel,
  * -1 = automatic (default: nontemporal loads when the per-step H+X stream
- * exceeds the Infinity Cache, plain loads otherwise -- bit-identical
- * arithmetic either way), else bit 0 =
- * zig-zag segment order on alternate blocks, bit 1 = nontemporal H/X loads.
+ * exceeds the Infinity Cache, plain loads otherwise -- the load policy never
+ * changes a result bit; the pipelined full-block step when B <= 512 and a
+ * channel's FDL holds <= 16384 bins, chosen per geometry, never by channel
+ * count, so channel shards stay bit-identical),
+ * else bit 0 = zig-zag segment order on alternate blocks, bit 1 =
+ * nontemporal H/X loads, bit 2 = no pipelined step (every call computes
+ * its pre_multiplied at block start, as the reference does).
  * Results agree within f32 rounding across variants. */
 int fftconv_set_kernel_variant(int variant);
 int fftconv_get_kernel_variant(void);
+/* Tuning knob (process-wide): FDL rows the pipelined step leaves to its
+ * stream waves while its first wave runs the transform chain; -1 = automatic
+ * (all of them: the first wave never streams).  Does not change results beyond
+ * f32 summation order. */
+int fftconv_set_pipeline_lag(int rows);
+int fftconv_get_pipeline_lag(void);
 
 /* ---- FFTConvolver (uniformly partitioned, zero latency) ---------------- */
 /* FFTConvolver::init, src/fft_convolver.rs:119-186.  NULL on error. */

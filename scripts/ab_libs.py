@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Same-process, interleaved A/B of several builds of libfftconv_amd.so on the
 cfg2 workload (methodology rule: never rank builds across processes/boxes).
+Each LIB may carry knobs applied before its timed runs: PATH,variant=6,lag=12.
 usage: ab_libs.py LIB1 LIB2 ... [--rounds R] [--steps K] [--channels C] [--block B] [--ir L]"""
 import argparse
 import ctypes as C
@@ -30,8 +31,14 @@ torch.cuda.set_stream(s)
 irs = shard.synth_irs(range(Cn), L)
 x = torch.from_numpy(shard.synth_dry(range(Cn), 16, B)).cuda()
 handles = []
-for path in a.libs:
-    lib = C.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+loaded = {}
+knobs = []
+for spec in a.libs:
+    path, *kv = spec.split(",")
+    knobs.append(dict(x.split("=") for x in kv))
+    if path not in loaded:
+        loaded[path] = C.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+    lib = loaded[path]
     lib.fftconv_uniform_init_batch.restype = C.c_void_p
     lib.fftconv_uniform_init_batch.argtypes = [C.c_int, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t]
     lib.fftconv_uniform_process_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]
@@ -42,6 +49,10 @@ res = [[] for _ in handles]
 k = 0
 for r in range(a.rounds):
     for idx, (lib, h, y) in enumerate(handles):
+        kn = knobs[idx]
+        if hasattr(lib, "fftconv_set_pipeline_lag"):
+            lib.fftconv_set_pipeline_lag(int(kn.get("lag", -1)))
+        lib.fftconv_set_kernel_variant(int(kn.get("variant", -1)))
         for _ in range(20):
             lib.fftconv_uniform_process_device(h, x[k % 16].data_ptr(), B, y[k % 16].data_ptr(), B, B, s.cuda_stream); k += 1
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -72,6 +72,10 @@ def main():
     p.add_argument("--configs", default="3,5")
     p.add_argument("--steps3", type=int, default=2048)
     p.add_argument("--steps5", type=int, default=512)
+    p.add_argument("--sweep", default="",
+                   help="cfg3 only: ';'-separated knob sets (e.g. 'lag=0;lag=32;variant=4') timed "
+                        "interleaved in this process, --rounds times")
+    p.add_argument("--rounds", type=int, default=4)
     a = p.parse_args()
     torch.cuda.set_device(0)
     s = torch.cuda.Stream()
@@ -83,6 +87,21 @@ def main():
         T = conv.tail_block_size
         samples = C * head * a.steps3
         per_sample = (uniform_bytes(head, T) + uniform_bytes(head, T) + uniform_bytes(T, L - 2 * T) * head / T) / head
+        if a.sweep:
+            sets = [dict(kv.split("=") for kv in part.split(",") if kv) for part in a.sweep.split(";")]
+            times = [[] for _ in sets]
+            for _ in range(a.rounds):
+                for j, kn in enumerate(sets):
+                    F.set_pipeline_lag(int(kn.get("lag", -1)))
+                    F.set_kernel_variant(int(kn.get("variant", -1)))
+                    t, ev = run(conv, C, head, head, a.steps3, 2 * T // head, 64, s, batched=True)
+                    times[j].append(t)
+            F.set_pipeline_lag(-1)
+            F.set_kernel_variant(-1)
+            for kn, ts in zip(sets, times):
+                t = sorted(ts)[len(ts) // 2]
+                out.append({"config": "cfg3 sweep", "knobs": kn, "MSamples_s": round(samples / t / 1e6, 2),
+                            "us_per_step": round(t / a.steps3 * 1e6, 3)})
         for batched in (False, True):
             t, ev = run(conv, C, head, head, a.steps3, 2 * T // head, 64, s, batched=batched)
             out.append({"config": "cfg3 TwoStageFFTConvolver", "host_loop": "C++ (process_device_steps)" if batched

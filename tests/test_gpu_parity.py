@@ -175,7 +175,7 @@ def test_uniform_vs_oracle(amd, oracle_mod, block, L, pattern):
     assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6])
 def test_uniform_kernel_variants(amd, oracle_mod, variant):
     """Every fused-kernel variant (zig-zag scan / nontemporal loads) against the
     oracle, with partial chunks, multi-block calls and an update in between."""
@@ -199,6 +199,71 @@ def test_uniform_kernel_variants(amd, oracle_mod, variant):
                 assert_close(got[c], refs[c].process(x[c]), what=f"variant {variant} chunk {j} ch {c}")
     finally:
         amd.set_kernel_variant(-1)
+
+
+@pytest.mark.parametrize("block,lag", [(2, -1), (8, 0), (32, 5), (64, -1), (128, 0), (128, 1000), (256, -1),
+                                       (256, 3), (512, -1), (512, 0)])
+def test_pipelined_step(amd, oracle_mod, block, lag):
+    """The pipelined full-block step (next block's pre_multiplied streamed
+    under the transform chain, FLAG_PRE) against the oracle: entry after a
+    full-block call, partial chunks in between (generic path, stored pre
+    reused), an update() (stored pre invalidated), reset(), and a response
+    shorter than three segments; the stream split is swept through `lag`."""
+    rng = np.random.default_rng(60 + block)
+    C, B = 3, block
+    L = 37 * B + 5
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    amd.set_pipeline_lag(lag)
+    try:
+        conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+        refs = [oracle_mod.FFTConvolver.init(hs[c], B, L) for c in range(C)]
+        chunks = [B] * 45 + [max(1, B // 3), B - max(1, B // 3)] + [B] * 6 + [B // 2 or 1] + [B] * 4 \
+            + [2 * B, B, B] + [B] * 3
+        for j, k in enumerate(chunks):
+            if j == 50:
+                hn = np.stack([ir(rng, 2 * B + 1) for _ in range(C)])  # act 3
+                conv.update(hn)
+                for c in range(C):
+                    refs[c].update(hn[c])
+            if j == 58:
+                hn = np.stack([ir(rng, B) for _ in range(C)])  # act 1
+                conv.update(hn)
+                for c in range(C):
+                    refs[c].update(hn[c])
+            x = np.stack([white(rng, k) for _ in range(C)])
+            got = conv.process(x)
+            for c in range(C):
+                assert_close(got[c], refs[c].process(x[c]), what=f"B={B} lag={lag} chunk {j} ch {c}")
+        assert conv.channel_state() == (refs[0].current, refs[0].active_seg_count, refs[0].fill)
+        conv.reset()
+        for c in range(C):
+            refs[c].reset()
+        for j in range(5):
+            x = np.stack([white(rng, B) for _ in range(C)])
+            got = conv.process(x)
+            for c in range(C):
+                assert_close(got[c], refs[c].process(x[c]), what=f"after reset, block {j}")
+    finally:
+        amd.set_pipeline_lag(-1)
+
+
+def test_pipelined_nan_block(amd, oracle_mod):
+    """A non-finite block on the pipelined path: zero output, the block kept in
+    the input buffer, state unchanged -- as the generic path and the oracle."""
+    rng = np.random.default_rng(70)
+    B, L = 256, 20 * 256
+    h = ir(rng, L)
+    conv = amd.FFTConvolver.init(h, B, L)
+    ref = oracle_mod.FFTConvolver.init(h, B, L)
+    for j in range(12):
+        x = white(rng, B)
+        if j == 6:
+            x[17] = np.nan
+        g, r = conv.process(x), ref.process(x)
+        assert np.array_equal(np.isnan(g), np.isnan(r))
+        m = ~np.isnan(r)
+        assert_close(g[m], r[m], what=f"block {j}")
+        assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
 
 
 def test_load_policy_is_bit_identical(amd):
