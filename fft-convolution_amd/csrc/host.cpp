@@ -660,6 +660,11 @@ struct CrossfadeCore {
     bool response_pending = false;
     hipStream_t stream = nullptr;
     Scratch scratch;
+    // crossfade pair launch (one FDL stream for A and B): allowed while A and B
+    // have had the same active_seg_count at every call; act[] as far as the
+    // host knows (-1: channels differ), sticky off once they disagree
+    long long act[2] = {-1, -1};
+    bool pair_ok = false;
 
     ~CrossfadeCore() {
         if (stream) {
@@ -680,6 +685,18 @@ struct CrossfadeCore {
         if (!a || !b) return fail(FFTCONV_E_NOMEM, "out of host memory");
         if (int r = a->clone_from(conv)) return r;
         if (int r = b->clone_from(conv)) return r;
+        // A and B start as copies: equal FDLs (FLAG_XSYNC), and one
+        // active_seg_count if every channel of `conv` has the same
+        if (C) {
+            std::vector<int4> st(C);
+            HIP_TRY(hipMemcpy(st.data(), a->state.p, C * sizeof(int4), hipMemcpyDeviceToHost));
+            bool uniform = true;
+            for (size_t c = 1; c < C; ++c) uniform = uniform && st[c].y == st[0].y;
+            act[0] = act[1] = uniform ? st[0].y : -1;
+            pair_ok = uniform && pair_supported(a->log2b, (int)a->S);
+            HIP_TRY(launch_state_flags(a->state.p, (int)C, FLAG_XSYNC, 0, stream));
+            HIP_TRY(launch_state_flags(b->state.p, (int)C, FLAG_XSYNC, 0, stream));
+        }
         stored_len = max_response_length;
         stored_stride = stored_len;
         if (int r = stored.alloc(C * stored_len)) return r;
@@ -698,12 +715,23 @@ struct CrossfadeCore {
     int swap_device(const float *src, size_t stride, size_t len, hipStream_t s) {
         if (xf.target == 0) {
             if (int r = b->update_device(src, stride, len, s)) return r;
+            note_update(1, len);
             xf.fade_into(1);
         } else {
             if (int r = a->update_device(src, stride, len, s)) return r;
+            note_update(0, len);
             xf.fade_into(0);
         }
         return FFTCONV_OK;
+    }
+
+    // FFTConvolver::update sets active_seg_count = ceil(len / B) on every
+    // channel (:199-204), unless the convolver is empty (:195-197)
+    void note_update(int which, size_t len) {
+        const UniformCore &u = which ? *b : *a;
+        if (u.ir_len == 0) return;
+        act[which] = (long long)ceil_div(len, u.B);
+        if (act[0] < 0 || act[0] != act[1]) pair_ok = false;
     }
 
     // Convolution::update (:51-64); host samples, channel c at src + c*stride (stride 0 = shared)
@@ -714,6 +742,7 @@ struct CrossfadeCore {
             UniformCore &t = xf.target == 0 ? *b : *a;
             if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
             if (int r = t.update_host(0, C, src, len, stride)) return r;
+            note_update(xf.target == 0 ? 1 : 0, len);
             xf.fade_into(xf.target == 0 ? 1 : 0);
             response_pending = false;
             return FFTCONV_OK;
@@ -778,7 +807,12 @@ struct CrossfadeCore {
             pa.job[1] = b->job(din, is, buf_b.p, m, m);
             pa.njobs = 2;
             pa.tw = a->tw.p;
-            HIP_TRY(launch_process(a->log2b, pa, (int)C, s));
+            // while A's and B's rings agree: one workgroup per channel reads
+            // the FDL once for both (bit-identical to the two-job launch)
+            if (pair_ok && pair_supported(a->log2b, (int)a->S))
+                HIP_TRY(launch_process_pair(a->log2b, pa, (int)C, s));
+            else
+                HIP_TRY(launch_process(a->log2b, pa, (int)C, s));
         }
         CrossfadeMixArgs x{};
         x.buf_a = buf_a.p; x.buf_b = buf_b.p; x.buf_stride = (long long)m;
@@ -816,6 +850,7 @@ struct CrossfadeCore {
         device = o.device; C = o.C; max_buffer_size = o.max_buffer_size;
         stored_len = o.stored_len; stored_stride = o.stored_stride;
         xf = o.xf; response_pending = o.response_pending;
+        act[0] = o.act[0]; act[1] = o.act[1]; pair_ok = o.pair_ok;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         a.reset(new (std::nothrow) UniformCore());
         b.reset(new (std::nothrow) UniformCore());
@@ -882,7 +917,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 7) return fail(FFTCONV_E_INVALID, "variant must be 0..7 (or -1 = auto)");
+    if (variant > 15) return fail(FFTCONV_E_INVALID, "variant must be 0..15 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }

@@ -198,6 +198,69 @@ __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const fl
     }
 }
 
+// Crossfade pair: the two convolvers' pre_multiplied from ONE read of the
+// shared FDL (A and B see the same input, so while their ring states agree
+// their FDL rows are equal).  Same row walk and per-accumulator order as
+// mac_rows (non-zig-zag), so each sum is bit-identical to the unpaired one.
+template <int LOG2B, int NT, bool NTL, class AccArr>
+__device__ __forceinline__ void mac_rows_pair(AccArr &accA, AccArr &accB, const float2 *HA, const float2 *HB,
+                                              const float2 *Xc, int S, int cur, int act, int f0, int g) {
+    using Gm = Geo<LOG2B, NT>;
+    constexpr int B = Gm::B, VEC = Gm::VEC, G = Gm::G, SPT = Gm::SPT;
+    constexpr int U = SPT == 1 ? 8 : (SPT == 2 ? 4 : 2);
+    constexpr int ROWB = B * (int)sizeof(float2);
+    constexpr bool UNIFORM = Gm::F >= 64;
+    using vec_t = typename VecT<VEC>::type;
+    const size_t bytes = (size_t)S * ROWB;
+    const RowStream ha(HA, bytes), hb(HB, bytes), xs(Xc, bytes);
+    const int lane_off = f0 * VEC * (int)sizeof(float2);
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+        accA[s].zero();
+        accB[s].zero();
+    }
+    int t = g;
+    int i = 1 + t;
+    int xi = (cur + i) % act;
+    for (; t + (U - 1) * G < act - 1; t += U * G) {
+        vec_t av[U][SPT], bv[U][SPT], xv[U][SPT];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ho = i * ROWB, xo = xi * ROWB;
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+                const int lo = lane_off + s * NT * VEC * (int)sizeof(float2);
+                av[u][s] = UNIFORM ? ha.ld<NTL>(lo, ho, (vec_t *)nullptr) : ha.ld<NTL>(lo + ho, 0, (vec_t *)nullptr);
+                bv[u][s] = UNIFORM ? hb.ld<NTL>(lo, ho, (vec_t *)nullptr) : hb.ld<NTL>(lo + ho, 0, (vec_t *)nullptr);
+                xv[u][s] = UNIFORM ? xs.ld<NTL>(lo, xo, (vec_t *)nullptr) : xs.ld<NTL>(lo + xo, 0, (vec_t *)nullptr);
+            }
+            i += G;
+            xi += G;
+            if (xi >= act) xi -= act;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+                accA[s].mac(av[u][s], xv[u][s]);
+                accB[s].mac(bv[u][s], xv[u][s]);
+            }
+    }
+    for (; t < act - 1; t += G) {
+        const int ho = i * ROWB, xo = xi * ROWB;
+#pragma unroll
+        for (int s = 0; s < SPT; ++s) {
+            const int lo = lane_off + s * NT * VEC * (int)sizeof(float2);
+            const vec_t x = UNIFORM ? xs.ld<NTL>(lo, xo, (vec_t *)nullptr) : xs.ld<NTL>(lo + xo, 0, (vec_t *)nullptr);
+            accA[s].mac(UNIFORM ? ha.ld<NTL>(lo, ho, (vec_t *)nullptr) : ha.ld<NTL>(lo + ho, 0, (vec_t *)nullptr), x);
+            accB[s].mac(UNIFORM ? hb.ld<NTL>(lo, ho, (vec_t *)nullptr) : hb.ld<NTL>(lo + ho, 0, (vec_t *)nullptr), x);
+        }
+        i += G;
+        xi += G;
+        if (xi >= act) xi -= act;
+    }
+}
+
 // Asynchronous global -> LDS copies (LDS-DMA, global_load_lds): lane l of a
 // wave writes dst + l*W for a wave-uniform dst, no VGPR destination, drained
 // by the next __syncthreads (s_waitcnt vmcnt(0) before s_barrier).
@@ -462,22 +525,19 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
 // overlap-add tail then runs out of LDS and registers only.
 // ---------------------------------------------------------------------------
 template <int LOG2B, int NT, bool ZZ, bool NTL>
-__global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
+__device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J, const size_t c, const int4 st,
+                                            unsigned char *smem) {
     using Gm = Geo<LOG2B, NT>;
     constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT;
     constexpr float invN = 1.0f / (float)(2 * B);
     using vec_t = typename VecT<VEC>::type;
 
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2 *bufA = reinterpret_cast<float2 *>(smem);
     float2 *bufB = bufA + B;
     vec_t *red = reinterpret_cast<vec_t *>(bufB + B);
     int &s_err = *reinterpret_cast<int *>(smem + Gm::lds_bytes - 16);
 
     const int tid = threadIdx.x;
-    const size_t c = blockIdx.x;
-    const ProcJob &J = a.job[blockIdx.y];
-    const int4 st = J.state[c];
     int cur = st.x;
     const int act = st.y;
     int fill = st.z;
@@ -700,6 +760,187 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
     }
     if (tid == 0) J.state[c] = make_int4(cur, act, fill, flags);
     if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
+}
+
+template <int LOG2B, int NT, bool ZZ, bool NTL>
+__global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const size_t c = blockIdx.x;
+    const ProcJob &J = a.job[blockIdx.y];
+    process_job<LOG2B, NT, ZZ, NTL>(a, J, c, J.state[c], smem);
+}
+
+// ---------------------------------------------------------------------------
+// Crossfade pair step: CrossfadeConvolver::process (src/crossfade_convolver.rs
+// :66-78) runs convolver_a and convolver_b on the same input block.  While
+// the two ring states agree (and FLAG_XSYNC says they always have), their
+// FDLs are equal row for row, so one workgroup per channel does both with
+// one FDL stream (H_A, H_B, X: 24 instead of 32 B per bin-row), one forward
+// transform written to both FDL rows, and the two C2Rs.  Each convolver's
+// arithmetic is exactly the unpaired kernel's (same sum order): pairing never
+// changes a result bit.  Any other call runs the two generic jobs in turn;
+// if the states disagree the channel drops FLAG_XSYNC for good.
+// B in [2, 512]; LDS: bufA | bufB | bufC | redA | redB | tw | H0a | H0b | ovA | ovB
+// ---------------------------------------------------------------------------
+template <int LOG2B, int NT>
+struct PairGeo {
+    using Gm = Geo<LOG2B, NT>;
+    static constexpr int B = Gm::B;
+    static constexpr size_t pair_bytes = 3 * 8 * (size_t)B + 2 * Gm::red_bytes + 16 * (size_t)B + 16 * (size_t)B +
+                                         8 * (size_t)B + 32;
+    static constexpr size_t lds_bytes = pair_bytes > Gm::lds_bytes ? pair_bytes : Gm::lds_bytes;
+};
+
+template <int LOG2B, int NT, bool NTL>
+__device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, int act, int flags,
+                                          unsigned char *smem) {
+    using Gm = Geo<LOG2B, NT>;
+    constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT;
+    constexpr float invN = 1.0f / (float)(2 * B);
+    using vec_t = typename VecT<VEC>::type;
+    static_assert(VEC == 2 && B <= 512, "pair step: 2 <= B <= 512");
+    float2 *bufA = reinterpret_cast<float2 *>(smem);
+    float2 *bufB = bufA + B;
+    float2 *bufC = bufB + B;
+    vec_t *redA = reinterpret_cast<vec_t *>(bufC + B);
+    vec_t *redB = reinterpret_cast<vec_t *>(reinterpret_cast<unsigned char *>(redA) + Gm::red_bytes);
+    float2 *twl = reinterpret_cast<float2 *>(reinterpret_cast<unsigned char *>(redB) + Gm::red_bytes);
+    float2 *h0[2] = {twl + 2 * B, twl + 3 * B};
+    float *ovl[2] = {reinterpret_cast<float *>(twl + 4 * B), reinterpret_cast<float *>(twl + 4 * B) + B};
+    int *s_err = reinterpret_cast<int *>(ovl[1] + B);  // [2]
+
+    const ProcJob *Js[2] = {&a.job[0], &a.job[1]};
+    const int tid = threadIdx.x;
+    const size_t rows = (size_t)Js[0]->S * B;
+    const float2 *Hc[2] = {Js[0]->H + c * rows, Js[1]->H + c * rows};
+    const float *inc = Js[0]->in + c * Js[0]->in_stride;
+    const int f0 = G > 1 ? tid % F : tid;
+    const int g = G > 1 ? (F >= 64 ? __builtin_amdgcn_readfirstlane(tid / F) : tid / F) : 0;
+    const bool owner = G > 1 ? tid < F : true;
+
+    // prologue (LDS-DMA): twiddles, both H[0], the packed block, both overlaps
+    dma_16b<NT>(twl, a.tw, 2 * B * (int)sizeof(float2));
+    dma_16b<NT>(h0[0], Hc[0], B * (int)sizeof(float2));
+    dma_16b<NT>(h0[1], Hc[1], B * (int)sizeof(float2));
+    dma_f32<NT>(reinterpret_cast<float *>(bufA), inc, B);
+    for (int m = B / 2 + tid; m < B; m += NT) bufA[m] = make_float2(0.f, 0.f);
+    dma_f32<NT>(ovl[0], Js[0]->overlap + c * B, B);
+    dma_f32<NT>(ovl[1], Js[1]->overlap + c * B, B);
+
+    // both pre_multiplied from one FDL stream (:258-269)
+    vec_t pacc[2][SPT];
+    {
+        AccT<VEC> accA[SPT], accB[SPT];
+        mac_rows_pair<LOG2B, NT, NTL>(accA, accB, Hc[0], Hc[1], Js[0]->X + c * rows, Js[0]->S, cur, act, f0, g);
+        if constexpr (G > 1) {
+            redA[g * F + f0] = accA[0].get(f0);
+            redB[g * F + f0] = accB[0].get(f0);
+            __syncthreads();
+            if (owner) {
+                vec_t p = redA[f0], q = redB[f0];
+#pragma unroll
+                for (int r = 1; r < G; ++r) {
+                    p = vadd(p, redA[r * F + f0]);
+                    q = vadd(q, redB[r * F + f0]);
+                }
+                pacc[0][0] = p;
+                pacc[1][0] = q;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+                pacc[0][s] = accA[s].get(f0 + s * NT);
+                pacc[1][s] = accB[s].get(f0 + s * NT);
+            }
+        }
+    }
+    if (tid < 2) s_err[tid] = 0;
+    __syncthreads();
+
+    // one R2C (:243-255), written to both FDL rows `current`
+    float2 *Z = lds_cfft<LOG2B, NT, false>(bufA, bufB, twl);
+    float2 *W = Z == bufA ? bufB : bufA;
+    float2 *XA = Js[0]->X + c * rows + (size_t)cur * B;
+    float2 *XB = Js[1]->X + c * rows + (size_t)cur * B;
+    for (int m = tid; m < B; m += NT) {
+        const float2 v = real_post<LOG2B, NT>(Z, m, twl);
+        bufC[m] = v;
+        XA[m] = v;
+        XB[m] = v;
+    }
+    __syncthreads();
+
+    for (int j = 0; j < 2; ++j) {
+        const ProcJob &J = *Js[j];
+        // conv = pre + X (.) H[0] (:270-275), then the C2R error check
+        if (owner) {
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+                const int f = f0 + s * NT;
+                const vec_t cv = slot_mac(pacc[j][s], reinterpret_cast<const vec_t *>(bufC)[f],
+                                          reinterpret_cast<const vec_t *>(h0[j])[f], f);
+                reinterpret_cast<vec_t *>(Z)[f] = cv;
+                if (f == 0 && !slot0_finite(cv)) s_err[j] = 1;
+            }
+        }
+        __syncthreads();
+        float *outc = J.out + c * J.out_stride;
+        if (!s_err[j]) {
+            for (int m = tid; m < B; m += NT) W[m] = real_pre<LOG2B, NT>(Z, m, twl);
+            __syncthreads();
+            const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, NT, true>(W, Z, twl));
+            float *ovc = J.overlap + c * B;
+            for (int k = tid; k < B; k += NT) {
+                outc[k] = y[k] * invN + ovl[j][k];  // :284-288
+                ovc[k] = y[B + k] * invN;            // :297-298
+            }
+            if (tid == 0) J.state[c] = make_int4(cur > 0 ? cur - 1 : act - 1, act, 0, (flags & ~FLAG_INBUF) ^ FLAG_REV);
+        } else {
+            // output.fill(0); return (:278-281): block kept in the input buffer
+            float *ibc = J.inbuf + c * B;
+            for (int k = tid; k < B; k += NT) {
+                outc[k] = 0.f;
+                ibc[k] = inc[k];
+            }
+            if (owner) {
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) reinterpret_cast<vec_t *>(J.pre + c * B)[f0 + s * NT] = pacc[j][s];
+            }
+            if (tid == 0) J.state[c] = make_int4(cur, act, 0, flags | FLAG_INBUF);
+        }
+        __syncthreads();  // Z / W are reused by the next convolver
+    }
+}
+
+// the generic body for both jobs in turn, out of line: the rare fallback
+// keeps its registers out of the pair step's allocation
+template <int LOG2B, int NT, bool NTL>
+__device__ __attribute__((noinline)) void pair_fallback(const ProcArgs &a, size_t c, int4 sa, int4 sb,
+                                                        unsigned char *smem) {
+    process_job<LOG2B, NT, false, NTL>(a, a.job[0], c, sa, smem);
+    __syncthreads();
+    process_job<LOG2B, NT, false, NTL>(a, a.job[1], c, sb, smem);
+}
+
+// (2 waves/SIMD suffice: C workgroups of 3 streams x 8 rows x 16 B per lane
+// in flight; the rarely-taken generic fallback then needs no spills)
+template <int LOG2B, int NT, bool NTL>
+__global__ __launch_bounds__(NT, 2) void upols_pair_kernel(ProcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const size_t c = blockIdx.x;
+    int4 sa = a.job[0].state[c], sb = a.job[1].state[c];
+    constexpr int KEY = FLAG_INBUF | FLAG_REV | FLAG_PRE;
+    const bool same = sa.x == sb.x && sa.y == sb.y && sa.z == sb.z && ((sa.w ^ sb.w) & KEY) == 0;
+    if (same && (sa.w & sb.w & FLAG_XSYNC) && sa.y > 0 && sa.z == 0 && a.job[0].n == (1 << LOG2B) &&
+        !(sa.w & (FLAG_INBUF | FLAG_PRE)) && sa.x < sa.y) {
+        pair_step<LOG2B, NT, NTL>(a, c, sa.x, sa.y, sa.w, smem);
+        return;
+    }
+    if (!same) {  // the rings have diverged (a C2R error in one of them): never pair again
+        sa.w &= ~FLAG_XSYNC;
+        sb.w &= ~FLAG_XSYNC;
+    }
+    pair_fallback<LOG2B, NT, NTL>(a, c, sa, sb, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -942,7 +1183,55 @@ hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStre
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 7); }
+template <int LOG2B>
+static hipError_t launch_pair_t(const ProcArgs &a, int channels, hipStream_t s) {
+    if constexpr (LOG2B < 1 || LOG2B > 9) {
+        return hipErrorNotSupported;
+    } else {
+        constexpr int PNT = proc_nt(LOG2B);
+        using PG = PairGeo<LOG2B, PNT>;
+        const int var = pick_variant(a, channels, LOG2B);
+        if (var & (VARIANT_ZIGZAG | VARIANT_NOPAIR)) return hipErrorNotSupported;  // the pair scan is the plain order only
+        ProcArgs args = a;
+        args.pipe = 0;
+        args.lag = 0;
+        auto kern = (var & VARIANT_NT) ? upols_pair_kernel<LOG2B, PNT, true> : upols_pair_kernel<LOG2B, PNT, false>;
+        if (PG::lds_bytes > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)PG::lds_bytes);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(kern, dim3(channels), dim3(PNT), PG::lds_bytes, s, args);
+        return hipGetLastError();
+    }
+}
+
+bool pair_supported(int log2b, int S) {
+    // long FDLs only: there the step is HBM-bound and the shared stream saves
+    // a quarter of the bytes; short ones are latency-bound and run better as
+    // two pipelined workgroups
+    return log2b >= 1 && log2b <= 9 && ((long long)S << log2b) > 16384 &&
+           (g_variant == VARIANT_AUTO || !(g_variant & (VARIANT_ZIGZAG | VARIANT_NOPAIR)));
+}
+
+hipError_t launch_process_pair(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    if (a.njobs != 2) return hipErrorInvalidValue;
+    FFTCONV_DISPATCH(launch_pair_t, log2b, a, channels, s)
+}
+
+__global__ void state_flags_kernel(int4 *state, int channels, int set, int clear) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < channels) state[c].w = (state[c].w & ~clear) | set;
+}
+
+hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    hipLaunchKernelGGL(state_flags_kernel, dim3((channels + 255) / 256), dim3(256), 0, s, state, channels, set, clear);
+    return hipGetLastError();
+}
+
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 15); }
 void set_pipeline_lag(int rows) { g_lag = rows < 0 ? -1 : rows; }
 int get_pipeline_lag() { return g_lag; }
 int get_variant() { return g_variant == VARIANT_AUTO ? -1 : g_variant; }

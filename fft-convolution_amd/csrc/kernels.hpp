@@ -9,10 +9,11 @@ enum : int {
     FLAG_INBUF = 1,  // the HBM input buffer holds live samples
     FLAG_REV = 2,    // scan parity of the segment MAC (toggled per completed block)
     FLAG_PRE = 4,    // pre[] holds pre_multiplied of the block that starts at `current`
+    FLAG_XSYNC = 8,  // crossfade pair: this FDL has always equalled its partner's
 };
 
 // fused-kernel variants (bit mask): 1 = zig-zag segment scan, 2 = nontemporal H/X loads
-enum : int { VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_NOPIPE = 4, VARIANT_AUTO = 0x7fffffff };
+enum : int { VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_NOPIPE = 4, VARIANT_NOPAIR = 8, VARIANT_AUTO = 0x7fffffff };
 void set_variant(int v);
 int get_variant();
 void set_pipeline_lag(int rows);
@@ -102,6 +103,10 @@ hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStrea
 hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipStream_t s);
 hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStream_t s);
 hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s);
+// crossfade pair (A and B of one CrossfadeConvolver in one workgroup per channel)
+bool pair_supported(int log2b, int S);
+hipError_t launch_process_pair(int log2b, const ProcArgs &a, int channels, hipStream_t s);
+hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hipStream_t s);
 size_t process_lds_bytes(int log2b);
 
 constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)

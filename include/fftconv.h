@@ -63,10 +63,13 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
  * exceeds the Infinity Cache, plain loads otherwise -- the load policy never
  * changes a result bit; the pipelined full-block step when B <= 512 and a
  * channel's FDL holds <= 16384 bins, chosen per geometry, never by channel
- * count, so channel shards stay bit-identical),
+ * count, so channel shards stay bit-identical; for a CrossfadeConvolver
+ * with a longer FDL, one workgroup runs A and B on one FDL stream, which
+ * never changes a result bit),
  * else bit 0 = zig-zag segment order on alternate blocks, bit 1 =
  * nontemporal H/X loads, bit 2 = no pipelined step (every call computes
- * its pre_multiplied at block start, as the reference does).
+ * its pre_multiplied at block start, as the reference does), bit 3 = no
+ * crossfade pair launch (A and B stream the shared FDL separately).
  * Results agree within f32 rounding across variants. */
 int fftconv_set_kernel_variant(int variant);
 int fftconv_get_kernel_variant(void);

@@ -541,6 +541,60 @@ def test_crossfade_vs_oracle(amd, oracle_mod, B, L, every, xfade):
         assert conv.is_crossfading() == ref.is_crossfading()
 
 
+def _crossfade_pair_run(amd, oracle_mod, seed, lens, nan_at=None):
+    """Drive a paired (automatic) and an unpaired (variant bits 3+2) crossfade
+    batch through the same calls; returns both outputs and the oracle's."""
+    rng = np.random.default_rng(seed)
+    C, B, L = 3, 64, 20000  # S*B = 20032 bins: the pair launch applies
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    convs = [amd.CrossfadeConvolver.init(hs, B, L, channels=C) for _ in range(2)]
+    refs = [oracle_mod.CrossfadeConvolver.init(hs[c], B, L) for c in range(C)]
+    outs = [[], [], []]
+    try:
+        for i in range(36):
+            if i % 6 == 2:
+                hn = np.stack([ir(rng, lens[(i // 6) % len(lens)]) for _ in range(C)])
+                if nan_at is not None and i // 6 == nan_at:
+                    hn[1, 7] = np.nan
+                for cv in convs:
+                    cv.update(hn)
+                for c in range(C):
+                    refs[c].update(hn[c])
+            x = np.stack([white(rng, B) for _ in range(C)])
+            for k, cv in enumerate(convs):
+                amd.set_kernel_variant(-1 if k == 0 else 12)  # 12: no pair, no pipelined step
+                outs[k].append(cv.process(x))
+            amd.set_kernel_variant(-1)
+            outs[2].append(np.stack([refs[c].process(x[c]) for c in range(C)]))
+    finally:
+        amd.set_kernel_variant(-1)
+    return [np.concatenate(o, axis=1) for o in outs]
+
+
+@pytest.mark.parametrize("lens", [[20000, 19990, 19950], [20000, 12000, 20000]])
+def test_crossfade_pair_launch(amd, oracle_mod, lens):
+    """The crossfade pair launch (A and B of a channel in one workgroup, one
+    read of the shared FDL) is bit-identical to the two-job launch and matches
+    the oracle -- including after a response of another segment count makes
+    the rings diverge (pairing then stops for good)."""
+    paired, unpaired, ref = _crossfade_pair_run(amd, oracle_mod, 90 + len(set(lens)), lens)
+    assert np.array_equal(paired, unpaired)
+    for c in range(paired.shape[0]):
+        assert_close(paired[c], ref[c], what=f"ch {c}")
+
+
+def test_crossfade_pair_divergence_by_c2r_error(amd, oracle_mod):
+    """A response with a NaN makes one convolver's C2R fail on one channel
+    only: its ring stops while its partner's advances; the pair kernel must
+    notice, drop FLAG_XSYNC and fall back for that channel."""
+    paired, unpaired, ref = _crossfade_pair_run(amd, oracle_mod, 99, [20000], nan_at=1)
+    assert np.array_equal(paired, unpaired, equal_nan=True)
+    for c in range(paired.shape[0]):
+        m = ~np.isnan(ref[c])
+        assert np.array_equal(np.isnan(paired[c]), ~m)
+        assert_close(paired[c][m], ref[c][m], what=f"ch {c}")
+
+
 def test_crossfade_batch(amd, oracle_mod):
     rng = np.random.default_rng(31)
     C, B, L = 3, 128, 600
