@@ -790,6 +790,16 @@ struct CrossfadeCore {
         return FFTCONV_OK;
     }
 
+    CrossfadeMixArgs mix_args(float *dout, size_t os, size_t out_len) const {
+        CrossfadeMixArgs x{};
+        x.buf_a = buf_a.p; x.buf_b = buf_b.p; x.buf_stride = (long long)max_buffer_size;
+        x.out = dout; x.out_stride = (long long)os; x.n = (int)out_len;
+        x.approaching = xf.approaching ? 1 : 0; x.target = xf.target;
+        x.counter0 = xf.counter; x.fading = xf.fading_samples;
+        x.mix_value0 = xf.mix_value; x.step = xf.mix_value_step;
+        return x;
+    }
+
     // Convolution::process (:66-78)
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t out_len, hipStream_t s) {
         if (out_len > max_buffer_size) return fail(FFTCONV_E_INVALID, "output longer than max_buffer_size (index out of bounds)");
@@ -809,18 +819,17 @@ struct CrossfadeCore {
             pa.tw = a->tw.p;
             // while A's and B's rings agree: one workgroup per channel reads
             // the FDL once for both (bit-identical to the two-job launch)
-            if (pair_ok && pair_supported(a->log2b, (int)a->S))
+            pa.mix = mix_args(dout, os, out_len);
+            if (pair_ok && pair_supported(a->log2b, (int)a->S) && m == a->B && out_len > 0) {
+                // :72-77 in one launch: A, B and the mix (no buf_a / buf_b round trip)
+                pa.fuse_mix = 1;
                 HIP_TRY(launch_process_pair(a->log2b, pa, (int)C, s));
-            else
-                HIP_TRY(launch_process(a->log2b, pa, (int)C, s));
+                xf.advance(out_len);
+                return FFTCONV_OK;
+            }
+            HIP_TRY(launch_process(a->log2b, pa, (int)C, s));
         }
-        CrossfadeMixArgs x{};
-        x.buf_a = buf_a.p; x.buf_b = buf_b.p; x.buf_stride = (long long)m;
-        x.out = dout; x.out_stride = (long long)os; x.n = (int)out_len;
-        x.approaching = xf.approaching ? 1 : 0; x.target = xf.target;
-        x.counter0 = xf.counter; x.fading = xf.fading_samples;
-        x.mix_value0 = xf.mix_value; x.step = xf.mix_value_step;
-        HIP_TRY(launch_crossfade_mix(x, (int)C, s));                      // :75-77
+        HIP_TRY(launch_crossfade_mix(mix_args(dout, os, out_len), (int)C, s));  // :75-77
         xf.advance(out_len);
         return FFTCONV_OK;
     }

@@ -771,6 +771,62 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Crossfade mix (src/crossfade_convolver.rs:75-77 + Crossfader::mix :242-278
+// + RaisedCosineMixer :160-169), all channels in lockstep.  mix_value is
+// walked by the same sequential f32 additions the reference performs (once
+// per workgroup into LDS, or per sample for calls longer than 1024), so the
+// gains are bit-identical to a serial walk.
+// ---------------------------------------------------------------------------
+// Crossfader::mix for sample j of the call.  vtab (if given) holds the
+// sequential mix_value walk: vtab[k] = mix_value0 + step + ... (k adds).
+__device__ __forceinline__ float mix_sample(const CrossfadeMixArgs &a, int j, float va, float vb,
+                                            const float *vtab) {
+    if (!a.approaching) return a.target == 0 ? va : vb;
+    const long long cj = a.counter0 + j + 1;
+    if (cj <= 0) return a.target == 0 ? vb : va;                   // hold the previous target
+    if (a.fading >= 1 && cj >= a.fading) return a.target == 0 ? va : vb;  // reached (snap)
+    const long long inc = cj - (a.counter0 > 0 ? a.counter0 : 0);
+    float v;
+    if (vtab) {
+        v = vtab[inc];
+    } else {
+        v = a.mix_value0;
+        for (long long q = 0; q < inc; ++q) v = __fadd_rn(v, a.step);
+    }
+    const float PI_HALF = 3.14159265358979323846f * 0.5f;
+    const float rad = __fmul_rn(PI_HALF, v);
+    const float cs = cosf(rad);
+    const float g1 = __fmul_rn(cs, cs);
+    const float g2 = __fsub_rn(1.0f, g1);
+    return __fadd_rn(__fmul_rn(va, g1), __fmul_rn(vb, g2));
+}
+
+// the mix_value walk of one call (n + 1 entries), one thread, bit-identical
+// to the reference's per-sample `mix_value += step` (:259)
+__device__ __forceinline__ void mix_walk(const CrossfadeMixArgs &a, float *vtab) {
+    float v = a.mix_value0;
+    vtab[0] = v;
+    for (int k = 1; k <= a.n; ++k) {
+        v = __fadd_rn(v, a.step);
+        vtab[k] = v;
+    }
+}
+
+__global__ void crossfade_mix_kernel(CrossfadeMixArgs a) {
+    __shared__ float vtab[1025];
+    const size_t c = blockIdx.x;
+    const float *A = a.buf_a + c * a.buf_stride;
+    const float *Bv = a.buf_b + c * a.buf_stride;
+    float *o = a.out + c * a.out_stride;
+    const bool tab = a.approaching && a.n <= 1024;
+    if (tab) {
+        if (threadIdx.x == 0) mix_walk(a, vtab);
+        __syncthreads();
+    }
+    for (int j = threadIdx.x; j < a.n; j += blockDim.x) o[j] = mix_sample(a, j, A[j], Bv[j], tab ? vtab : nullptr);
+}
+
+// ---------------------------------------------------------------------------
 // Crossfade pair step: CrossfadeConvolver::process (src/crossfade_convolver.rs
 // :66-78) runs convolver_a and convolver_b on the same input block.  While
 // the two ring states agree (and FLAG_XSYNC says they always have), their
@@ -786,8 +842,9 @@ template <int LOG2B, int NT>
 struct PairGeo {
     using Gm = Geo<LOG2B, NT>;
     static constexpr int B = Gm::B;
+    // ... | s_err[2] (16 B) | A's output (B floats) | mix_value walk (B + 1 floats)
     static constexpr size_t pair_bytes = 3 * 8 * (size_t)B + 2 * Gm::red_bytes + 16 * (size_t)B + 16 * (size_t)B +
-                                         8 * (size_t)B + 32;
+                                         8 * (size_t)B + 16 + 4 * (size_t)B + 4 * ((size_t)B + 4);
     static constexpr size_t lds_bytes = pair_bytes > Gm::lds_bytes ? pair_bytes : Gm::lds_bytes;
 };
 
@@ -808,6 +865,9 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
     float2 *h0[2] = {twl + 2 * B, twl + 3 * B};
     float *ovl[2] = {reinterpret_cast<float *>(twl + 4 * B), reinterpret_cast<float *>(twl + 4 * B) + B};
     int *s_err = reinterpret_cast<int *>(ovl[1] + B);  // [2]
+    float *ya = reinterpret_cast<float *>(s_err + 4);   // A's output, for the fused mix
+    float *vtab = ya + B;                               // mix_value walk
+    const bool fuse = a.fuse_mix != 0;
 
     const ProcJob *Js[2] = {&a.job[0], &a.job[1]};
     const int tid = threadIdx.x;
@@ -826,6 +886,8 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
     for (int m = B / 2 + tid; m < B; m += NT) bufA[m] = make_float2(0.f, 0.f);
     dma_f32<NT>(ovl[0], Js[0]->overlap + c * B, B);
     dma_f32<NT>(ovl[1], Js[1]->overlap + c * B, B);
+    // the crossfader's mix_value walk (one lane; hides under the FDL stream)
+    if (fuse && a.mix.approaching && tid == 0) mix_walk(a.mix, vtab);
 
     // both pre_multiplied from one FDL stream (:258-269)
     vec_t pacc[2][SPT];
@@ -891,15 +953,24 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
             const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, NT, true>(W, Z, twl));
             float *ovc = J.overlap + c * B;
             for (int k = tid; k < B; k += NT) {
-                outc[k] = y[k] * invN + ovl[j][k];  // :284-288
-                ovc[k] = y[B + k] * invN;            // :297-298
+                const float v = y[k] * invN + ovl[j][k];  // :284-288
+                ovc[k] = y[B + k] * invN;                  // :297-298
+                if (!fuse) {
+                    outc[k] = v;
+                } else if (j == 0) {
+                    ya[k] = v;
+                } else if (k < a.mix.n) {                  // crossfade_convolver.rs:75-77
+                    a.mix.out[c * a.mix.out_stride + k] = mix_sample(a.mix, k, ya[k], v, vtab);
+                }
             }
             if (tid == 0) J.state[c] = make_int4(cur > 0 ? cur - 1 : act - 1, act, 0, (flags & ~FLAG_INBUF) ^ FLAG_REV);
         } else {
             // output.fill(0); return (:278-281): block kept in the input buffer
             float *ibc = J.inbuf + c * B;
             for (int k = tid; k < B; k += NT) {
-                outc[k] = 0.f;
+                if (!fuse) outc[k] = 0.f;
+                else if (j == 0) ya[k] = 0.f;
+                else if (k < a.mix.n) a.mix.out[c * a.mix.out_stride + k] = mix_sample(a.mix, k, ya[k], 0.f, vtab);
                 ibc[k] = inc[k];
             }
             if (owner) {
@@ -920,6 +991,13 @@ __device__ __attribute__((noinline)) void pair_fallback(const ProcArgs &a, size_
     process_job<LOG2B, NT, false, NTL>(a, a.job[0], c, sa, smem);
     __syncthreads();
     process_job<LOG2B, NT, false, NTL>(a, a.job[1], c, sb, smem);
+    if (a.fuse_mix) {  // the jobs wrote buf_a / buf_b (this workgroup's own stores)
+        __threadfence_block();
+        __syncthreads();
+        const float *A = a.mix.buf_a + c * a.mix.buf_stride, *Bv = a.mix.buf_b + c * a.mix.buf_stride;
+        for (int k = threadIdx.x; k < a.mix.n; k += NT)
+            a.mix.out[c * a.mix.out_stride + k] = mix_sample(a.mix, k, A[k], Bv[k], nullptr);
+    }
 }
 
 // (2 waves/SIMD suffice: C workgroups of 3 streams x 8 rows x 16 B per lane
@@ -1008,44 +1086,6 @@ __global__ void twostage_accum_kernel(TwoStageAccumArgs a) {
         v += p1[j];
         o[j] = v;
         ti[j] = x[j];
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Crossfade mix (src/crossfade_convolver.rs:75-77 + Crossfader::mix :242-278
-// + RaisedCosineMixer :160-169), all channels in lockstep.  Each sample
-// recomputes its mix_value by the same sequential f32 additions the
-// reference performs, so the gains are bit-identical to a serial walk.
-// ---------------------------------------------------------------------------
-__global__ void crossfade_mix_kernel(CrossfadeMixArgs a) {
-    const size_t c = blockIdx.x;
-    const float *A = a.buf_a + c * a.buf_stride;
-    const float *Bv = a.buf_b + c * a.buf_stride;
-    float *o = a.out + c * a.out_stride;
-    const float PI_HALF = 3.14159265358979323846f * 0.5f;
-    for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
-        const float va = A[j], vb = Bv[j];
-        float r;
-        if (!a.approaching) {
-            r = a.target == 0 ? va : vb;
-        } else {
-            const long long cj = a.counter0 + j + 1;
-            if (cj <= 0) {
-                r = a.target == 0 ? vb : va;                // hold the previous target
-            } else if (a.fading >= 1 && cj >= a.fading) {
-                r = a.target == 0 ? va : vb;                // reached (snap)
-            } else {
-                const long long inc = cj - (a.counter0 > 0 ? a.counter0 : 0);
-                float v = a.mix_value0;
-                for (long long q = 0; q < inc; ++q) v = __fadd_rn(v, a.step);
-                const float rad = __fmul_rn(PI_HALF, v);
-                const float cs = cosf(rad);
-                const float g1 = __fmul_rn(cs, cs);
-                const float g2 = __fsub_rn(1.0f, g1);
-                r = __fadd_rn(__fmul_rn(va, g1), __fmul_rn(vb, g2));
-            }
-        }
-        o[j] = r;
     }
 }
 

@@ -43,6 +43,23 @@ struct ProcJob {
     int n;                 // output samples this call
 };
 
+// Crossfader::mix over one call's samples (src/crossfade_convolver.rs:242-278),
+// the crossfader state at the start of the call.
+struct CrossfadeMixArgs {
+    const float *buf_a;
+    const float *buf_b;
+    long long buf_stride;
+    float *out;
+    long long out_stride;
+    int n;
+    int approaching;       // FadingState::Approaching
+    int target;            // 0 = A, 1 = B
+    long long counter0;
+    long long fading;
+    float mix_value0;
+    float step;
+};
+
 // Up to two jobs of the same block size in one launch (grid.y = job): the
 // two-stage head and tail0 run together on the same input block.
 struct ProcArgs {
@@ -51,6 +68,8 @@ struct ProcArgs {
     int njobs;
     int pipe;              // pipelined full-block step allowed (B <= 512)
     int lag;               // pipelined step: FDL rows wave 0 leaves to the stream waves
+    int fuse_mix;          // crossfade pair launch: mix A and B into mix.out in-kernel
+    CrossfadeMixArgs mix;  // (buf_a / buf_b unused then)
 };
 
 struct IrArgs {
@@ -83,20 +102,6 @@ struct TwoStageAccumArgs {
     int cnt;               // samples in the sub-chunk
 };
 
-struct CrossfadeMixArgs {
-    const float *buf_a;
-    const float *buf_b;
-    long long buf_stride;
-    float *out;
-    long long out_stride;
-    int n;
-    int approaching;       // FadingState::Approaching
-    int target;            // 0 = A, 1 = B
-    long long counter0;
-    long long fading;
-    float mix_value0;
-    float step;
-};
 
 hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s);
