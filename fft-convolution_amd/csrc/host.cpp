@@ -135,6 +135,13 @@ struct UniformCore {
     DevPtr<int4> state;
     hipStream_t stream = nullptr;
     Scratch scratch;
+    // lookahead (la.hpp): standalone batches only (la_ok, set before init)
+    bool la_ok = false;
+    int la_W = 0;                 // anchor workgroups per channel, 0 = off
+    DevPtr<float2> laP;           // [C][2][LA_D][la_W][B] far-row windows
+    unsigned long long la_t = 0;  // lookahead launches so far (stagger clock)
+    int la_seq = 1;               // launch tag, alternating 1 / 2
+    bool la_all = true;           // next lookahead launch re-anchors every channel
 
     ~UniformCore() {
         if (stream) {
@@ -164,6 +171,10 @@ struct UniformCore {
         if (int r = state.alloc(C)) return r;
         if (int r = tw.alloc(2 * B)) return r;
         if (int r = staging.alloc(C * ir_len)) return r;  // update() never allocates
+        la_W = la_ok ? la_parts(log2b, (int)S) : 0;
+        if (la_W) {
+            if (int r = laP.alloc(C * 2 * (size_t)la_window() * (size_t)la_W * B)) return r;
+        }
         // twiddles W_N^k in double, rounded to f32
         std::vector<float2> t(2 * B);
         const size_t N = 2 * B;
@@ -196,6 +207,7 @@ struct UniformCore {
         a.len_data = (long long)len_data; a.len_active = (long long)len_active;
         a.tw = tw.p; a.S = (int)S; a.chan0 = (int)chan0; a.update_state = update_state ? 1 : 0;
         HIP_TRY(launch_ir_segments(log2b, a, (int)nch, s));
+        if (update_state) la_all = true;  // the updated channels dropped their windows
         return FFTCONV_OK;
     }
 
@@ -257,6 +269,7 @@ struct UniformCore {
         if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), s));
         if (pre.n) HIP_TRY(hipMemsetAsync(pre.p, 0, pre.bytes(), s));
         HIP_TRY(launch_reset_state(state.p, (int)C, s));
+        la_all = true;
         return FFTCONV_OK;
     }
 
@@ -275,6 +288,25 @@ struct UniformCore {
         a.job[0] = job(din, is, dout, os, n);
         a.tw = tw.p;
         a.njobs = 1;
+        if (la_W && n == B && la_parts(log2b, (int)S) == la_W) {
+            // lookahead launch: C step workgroups behind this launch's anchors
+            // (every channel on entry, else the stagger class (c - t) % D == 0)
+            const size_t D = (size_t)la_window();
+            const size_t t0 = (size_t)(la_t % D);
+            const size_t nch = la_all ? C : (C > t0 ? (C - t0 + D - 1) / D : 0);
+            a.laP = laP.p;
+            a.la_W = la_W;
+            a.la_all = la_all ? 1 : 0;
+            a.la_t = (int)t0;
+            a.la_seq = la_seq;
+            a.la_nanchor = (int)(nch * (size_t)la_W);
+            HIP_TRY(launch_process_la(log2b, a, (int)C, s));
+            ++la_t;
+            la_seq = 3 - la_seq;
+            la_all = false;
+            return FFTCONV_OK;
+        }
+        if (la_W) la_all = true;  // this launch drops every window
         HIP_TRY(launch_process(log2b, a, (int)C, s));
         return FFTCONV_OK;
     }
@@ -312,6 +344,8 @@ struct UniformCore {
         if (int r = cp(overlap, o.overlap)) return r;
         if (int r = cp(inbuf, o.inbuf)) return r;
         if (int r = cp(state, o.state)) return r;
+        if (int r = cp(laP, o.laP)) return r;
+        la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
         if (int r = staging.alloc(o.staging.n)) return r;
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
@@ -926,7 +960,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 15) return fail(FFTCONV_E_INVALID, "variant must be 0..15 (or -1 = auto)");
+    if (variant > 63) return fail(FFTCONV_E_INVALID, "variant must be 0..63 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }
@@ -950,6 +984,7 @@ fftconv_uniform *fftconv_uniform_init_batch(int device, size_t channels, const f
     set_error("");
     auto *h = new (std::nothrow) fftconv_uniform();
     if (!h) { set_error("out of host memory"); return nullptr; }
+    h->core.la_ok = true;
     int r = h->core.init(device, channels, responses, response_len, response_stride, max_block_size,
                          max_response_length);
     return make_or_null(r, h);
@@ -1019,6 +1054,7 @@ int fftconv_uniform_synchronize(fftconv_uniform *h) {
     return FFTCONV_OK;
 }
 size_t fftconv_uniform_channels(const fftconv_uniform *h) { return h ? h->core.C : 0; }
+int fftconv_uniform_lookahead_parts(const fftconv_uniform *h) { return h ? h->core.la_W : 0; }
 size_t fftconv_uniform_block_size(const fftconv_uniform *h) { return h ? h->core.B : 0; }
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h) { return h ? h->core.S : 0; }
 int fftconv_uniform_channel_state(const fftconv_uniform *h, size_t channel, size_t out3[3]) {

@@ -102,6 +102,10 @@ __device__ __forceinline__ float4 slot_mac(float4 pre, float4 x, float4 h, int s
 __device__ __forceinline__ float2 slot_mac(float2 pre, float2 x, float2 h, int) {
     return make_float2(fmaf(x.x, h.x, pre.x), fmaf(x.y, h.y, pre.y));
 }
+// a state word written by a non-lookahead step: no live window, this launch's tag
+__device__ __forceinline__ int la_clear(int flags, const ProcArgs &a) {
+    return (flags & ~(LA_MASK | SEQ_MASK)) | (a.la_seq << SEQ_SHIFT);
+}
 __device__ __forceinline__ bool slot0_finite(float4 v) { return isfinite(v.x) && isfinite(v.y); }
 __device__ __forceinline__ bool slot0_finite(float2 v) { return isfinite(v.x) && isfinite(v.y); }
 
@@ -494,7 +498,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     }
     __syncthreads();
     if (s_err) {
-        if (tid == 0) J.state[c] = make_int4(cur, act, 0, flags | FLAG_INBUF);
+        if (tid == 0) J.state[c] = make_int4(cur, act, 0, la_clear(flags | FLAG_INBUF, a));
         return;
     }
     // next block's pre: every lane parks its partial sums in LDS (the whole
@@ -511,7 +515,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             for (int r = (w == 0 ? 1 : 0); r < RPW; ++r) p = vadd(p, red[w * SPL * 64 + base + r * F]);
         reinterpret_cast<float4 *>(prec)[f] = p;
     }
-    if (tid == 0) J.state[c] = make_int4(curp, act, 0, ((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE);
+    if (tid == 0) J.state[c] = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
 }
 
 // ---------------------------------------------------------------------------
@@ -758,9 +762,11 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
 #pragma unroll
         for (int s = 0; s < SPT; ++s) reinterpret_cast<vec_t *>(prec)[f0 + s * NT] = pacc[s];
     }
-    if (tid == 0) J.state[c] = make_int4(cur, act, fill, flags);
+    if (tid == 0) J.state[c] = make_int4(cur, act, fill, la_clear(flags, a));
     if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
 }
+
+#include "la.hpp"
 
 template <int LOG2B, int NT, bool ZZ, bool NTL>
 __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
@@ -963,7 +969,7 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
                     a.mix.out[c * a.mix.out_stride + k] = mix_sample(a.mix, k, ya[k], v, vtab);
                 }
             }
-            if (tid == 0) J.state[c] = make_int4(cur > 0 ? cur - 1 : act - 1, act, 0, (flags & ~FLAG_INBUF) ^ FLAG_REV);
+            if (tid == 0) J.state[c] = make_int4(cur > 0 ? cur - 1 : act - 1, act, 0, la_clear((flags & ~FLAG_INBUF) ^ FLAG_REV, a));
         } else {
             // output.fill(0); return (:278-281): block kept in the input buffer
             float *ibc = J.inbuf + c * B;
@@ -977,7 +983,7 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
 #pragma unroll
                 for (int s = 0; s < SPT; ++s) reinterpret_cast<vec_t *>(J.pre + c * B)[f0 + s * NT] = pacc[j][s];
             }
-            if (tid == 0) J.state[c] = make_int4(cur, act, 0, flags | FLAG_INBUF);
+            if (tid == 0) J.state[c] = make_int4(cur, act, 0, la_clear(flags | FLAG_INBUF, a));
         }
         __syncthreads();  // Z / W are reused by the next convolver
     }
@@ -1047,7 +1053,7 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
         }
         if (tid == 0) {
             a.state[c].y = (int)active;
-            a.state[c].w &= ~FLAG_PRE;  // the stored pre used the old response
+            a.state[c].w &= ~(FLAG_PRE | LA_MASK | SEQ_MASK);  // the stored pre / window used the old response
         }
     }
     if (i >= active) {  // :224-226
@@ -1206,6 +1212,55 @@ hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_
     FFTCONV_DISPATCH(launch_process_t, log2b, a, channels, s)
 }
 
+// Lookahead geometry policy: block sizes whose row is whole waves of float4
+// slots (128..512) and FDLs long enough that the far rows dominate.  A
+// function of (B, S) only, never of the channel count.
+int la_parts(int log2b, int S) {
+    if (log2b < 7 || log2b > 9) return 0;
+    if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NOLA)) return 0;
+    if (S < 3 * (LA_D + 1)) return 0;
+    const int lpw = LA_NT / ((1 << log2b) / 2);
+    return LA_NG / lpw;
+}
+int la_window() { return LA_D; }
+
+template <int LOG2B>
+static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
+    if constexpr (LOG2B < 7 || LOG2B > 9) {
+        return hipErrorNotSupported;
+    } else {
+        using LG = LaGeo<LOG2B>;
+        constexpr size_t gen = Geo<LOG2B, LA_NT>::lds_bytes;
+        constexpr size_t lds0 = LG::step_bytes > LG::anchor_bytes ? LG::step_bytes : LG::anchor_bytes;
+        constexpr size_t lds = lds0 > gen ? lds0 : gen;
+        if (a.la_W * LG::LPW > LA_NG || a.la_W < 1) return hipErrorInvalidValue;
+        // the far-row streams: nontemporal once the whole H + FDL working set
+        // (re-read every D steps) exceeds the Infinity Cache
+        const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
+        const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
+        auto kern = ntl ? upols_la_kernel<LOG2B, true> : upols_la_kernel<LOG2B, false>;
+        ProcArgs args = a;
+        args.pipe = 0;
+        args.lag = 0;
+        if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) {
+            args.la_all = -1;  // no anchors: every eligible step sums all its rows
+            args.la_nanchor = 0;
+        }
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(kern, dim3(args.la_nanchor + channels), dim3(LA_NT), lds, s, args);
+        return hipGetLastError();
+    }
+}
+
+hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    if (a.njobs != 1 || !a.laP) return hipErrorInvalidValue;
+    FFTCONV_DISPATCH(launch_la_t, log2b, a, channels, s)
+}
+
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s) {
     if (channels <= 0 || a.S <= 0) return hipSuccess;
     FFTCONV_DISPATCH(launch_ir_t, log2b, a, channels, s)
@@ -1271,7 +1326,7 @@ hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hip
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 15); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 63); }
 void set_pipeline_lag(int rows) { g_lag = rows < 0 ? -1 : rows; }
 int get_pipeline_lag() { return g_lag; }
 int get_variant() { return g_variant == VARIANT_AUTO ? -1 : g_variant; }

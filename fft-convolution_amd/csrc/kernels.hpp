@@ -10,10 +10,25 @@ enum : int {
     FLAG_REV = 2,    // scan parity of the segment MAC (toggled per completed block)
     FLAG_PRE = 4,    // pre[] holds pre_multiplied of the block that starts at `current`
     FLAG_XSYNC = 8,  // crossfade pair: this FDL has always equalled its partner's
+    // lookahead (time-blocked FDL, see la.hpp): an anchor's window of far-row
+    // partial sums is live (FLAG_LA) in P window FLAG_PWIN; bits 8-11 = steps of
+    // the window consumed, 12-15 = window length; bits 16-17 = the launch
+    // sequence tag of the last process launch that wrote this state word
+    FLAG_LA = 16,
+    FLAG_PWIN = 32,
+    LA_J_SHIFT = 8,
+    LA_D_SHIFT = 12,
+    SEQ_SHIFT = 16,
+    LA_MASK = FLAG_LA | (15 << LA_J_SHIFT) | (15 << LA_D_SHIFT),
+    SEQ_MASK = 3 << SEQ_SHIFT,
 };
 
 // fused-kernel variants (bit mask): 1 = zig-zag segment scan, 2 = nontemporal H/X loads
-enum : int { VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_NOPIPE = 4, VARIANT_NOPAIR = 8, VARIANT_AUTO = 0x7fffffff };
+enum : int {
+    VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_NOPIPE = 4, VARIANT_NOPAIR = 8, VARIANT_NOLA = 16,
+    VARIANT_LAFULL = 32,  // lookahead launches without anchors: every step sums all rows itself (tests)
+    VARIANT_AUTO = 0x7fffffff
+};
 void set_variant(int v);
 int get_variant();
 void set_pipeline_lag(int rows);
@@ -70,6 +85,13 @@ struct ProcArgs {
     int lag;               // pipelined step: FDL rows wave 0 leaves to the stream waves
     int fuse_mix;          // crossfade pair launch: mix A and B into mix.out in-kernel
     CrossfadeMixArgs mix;  // (buf_a / buf_b unused then)
+    // lookahead launch (launch_process_la; job[0] only)
+    float2 *laP;           // [C][2 windows][LA_D][la_W][B] far-row partial sums
+    int la_W;              // anchor workgroups per channel
+    int la_nanchor;        // anchor workgroups at the front of the grid
+    int la_all;            // 1: every channel is scheduled for an anchor (entry launch); -1: none is
+    int la_t;              // launch counter mod LA_D: channel c anchors when (c - t) % LA_D == 0
+    int la_seq;            // 1 or 2, alternating per lookahead launch; 0 in every other launch
 };
 
 struct IrArgs {
@@ -113,6 +135,10 @@ bool pair_supported(int log2b, int S);
 hipError_t launch_process_pair(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hipStream_t s);
 size_t process_lds_bytes(int log2b);
+// lookahead: anchor workgroups per channel for this geometry, 0 = not used
+int la_parts(int log2b, int S);
+int la_window();  // LA_D
+hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 
 constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)
 

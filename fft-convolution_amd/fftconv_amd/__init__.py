@@ -60,6 +60,7 @@ SIGNATURES = {
     "fftconv_uniform_destroy": (None, [_vp]),
     "fftconv_uniform_synchronize": (_i, [_vp]),
     "fftconv_uniform_channels": (_sz, [_vp]),
+    "fftconv_uniform_lookahead_parts": (_i, [_vp]),
     "fftconv_uniform_block_size": (_sz, [_vp]),
     "fftconv_uniform_seg_count": (_sz, [_vp]),
     "fftconv_uniform_channel_state": (_i, [_vp, _sz, C.POINTER(_sz)]),
@@ -293,6 +294,10 @@ class FFTConvolver(_Base):
     @property
     def seg_count(self) -> int:
         return int(lib().fftconv_uniform_seg_count(self._h))
+
+    def lookahead_parts(self) -> int:
+        """Anchor workgroups per channel of the lookahead step (0 = not used)."""
+        return int(lib().fftconv_uniform_lookahead_parts(self._h))
 
     def channel_state(self, channel: int = 0):
         """(current, active_seg_count, input_buffer_fill)."""

@@ -69,7 +69,15 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
  * else bit 0 = zig-zag segment order on alternate blocks, bit 1 =
  * nontemporal H/X loads, bit 2 = no pipelined step (every call computes
  * its pre_multiplied at block start, as the reference does), bit 3 = no
- * crossfade pair launch (A and B stream the shared FDL separately).
+ * crossfade pair launch (A and B stream the shared FDL separately), bit 4 =
+ * no lookahead step (see below), bit 5 = lookahead launches without anchors
+ * (every full block sums all its FDL rows itself; bit-identical to the
+ * lookahead path, for tests).
+ * Lookahead (automatic for standalone FFTConvolver batches with
+ * 128 <= B <= 512 and >= 27 segments): the far FDL rows' terms of the next
+ * 8 full blocks are summed ahead in one pass over H and the FDL, so a
+ * full-block call streams ~1/8 of the rows; its summation order does not
+ * depend on the channel index, the shard or the call history.
  * Results agree within f32 rounding across variants. */
 int fftconv_set_kernel_variant(int variant);
 int fftconv_get_kernel_variant(void);
@@ -128,6 +136,8 @@ fftconv_uniform *fftconv_uniform_clone(const fftconv_uniform *h);
 void fftconv_uniform_destroy(fftconv_uniform *h);
 int fftconv_uniform_synchronize(fftconv_uniform *h);
 size_t fftconv_uniform_channels(const fftconv_uniform *h);
+/* anchor workgroups per channel of the lookahead step, 0 = not used */
+int fftconv_uniform_lookahead_parts(const fftconv_uniform *h);
 size_t fftconv_uniform_block_size(const fftconv_uniform *h);   /* next_power_of_two(max_block_size) */
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h);
 /* copies {current, active_seg_count, input_buffer_fill} of one channel */

@@ -1,0 +1,174 @@
+"""The lookahead step (fft-convolution_amd/csrc/la.hpp) on the device.
+
+FFTConvolver::process (src/fft_convolver.rs:229-309) for a full block with
+the FDL sum re-associated in time: anchors sum the far rows' terms of the
+next 8 blocks ahead.  Checked against the oracle (tolerance REL_TOL, as every
+parity test), and for the property the design rests on -- the summation
+order is canonical, so the bits do not depend on a channel's stagger phase,
+its index, the shard it sits in, or whether a step was served from a window
+or summed all its rows itself (VARIANT_LAFULL)."""
+import numpy as np
+import pytest
+
+from common import assert_close, ir, white
+
+pytestmark = pytest.mark.gpu
+
+NOLA, LAFULL = 16, 32
+
+
+def _refs(oracle_mod, hs, B, L):
+    return [oracle_mod.FFTConvolver.init(hs[c], B, L) for c in range(hs.shape[0])]
+
+
+@pytest.mark.parametrize("B", [128, 256, 512])
+def test_lookahead_vs_oracle(amd, oracle_mod, B):
+    """Entry, > 3 windows per channel (the FDL ring wraps), a batch update,
+    partial and multi-block calls in between, a channel update and reset."""
+    rng = np.random.default_rng(300 + B)
+    C, L = 6, 40 * B + 3
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    assert conv.lookahead_parts() > 0
+    refs = _refs(oracle_mod, hs, B, L)
+    S = refs[0].seg_count
+    chunks = [B] * (2 * S) + [B // 3, B - B // 3] + [B] * 20 + [2 * B] + [B] * 20 + [B // 2] + [B] * 12
+    for j, k in enumerate(chunks):
+        if j == S + 5:
+            hn = np.stack([ir(rng, L - 7 * B) for _ in range(C)])  # act shrinks, ring indexing mod act
+            conv.update(hn)
+            for c in range(C):
+                refs[c].update(hn[c])
+        if j == 2 * S + 30:
+            hn = ir(rng, L)
+            conv.update_channel(4, hn)
+            refs[4].update(hn)
+        x = np.stack([white(rng, k) for _ in range(C)])
+        got = conv.process(x)
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"B={B} chunk {j} ch {c}")
+    for c in range(C):
+        assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
+    conv.reset()
+    for c in range(C):
+        refs[c].reset()
+    for j in range(12):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        got = conv.process(x)
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"after reset, block {j}")
+
+
+def test_lookahead_phase_independent(amd):
+    """13 identical channels sit at 8 different stagger phases (and anchor at
+    different launches): every channel's output is bit-identical, through a
+    partial call and a re-entry."""
+    rng = np.random.default_rng(310)
+    C, B, L = 13, 256, 50 * 256
+    h = ir(rng, L)
+    conv = amd.FFTConvolver.init(np.tile(h, (C, 1)), B, L, channels=C)
+    assert conv.lookahead_parts() > 0
+    for j in range(150):
+        k = 100 if j == 70 else (B - 100 if j == 71 else B)
+        x = np.tile(white(rng, k), (C, 1))
+        y = conv.process(x)
+        for c in range(1, C):
+            assert np.array_equal(y[c], y[0]), (j, c)
+
+
+def test_lookahead_window_equals_full_sum(amd):
+    """Steps served from anchor windows give the same bits as steps that sum
+    every FDL row themselves (VARIANT_LAFULL), and the variant without the
+    lookahead step agrees within f32 rounding."""
+    rng = np.random.default_rng(320)
+    C, B, L = 5, 256, 60 * 256 + 11
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    xs = [np.stack([white(rng, B) for _ in range(C)]) for _ in range(140)]
+    outs = {}
+    for v in (-1, LAFULL, NOLA):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+            outs[v] = np.concatenate([conv.process(x) for x in xs], axis=1)
+        finally:
+            amd.set_kernel_variant(-1)
+    assert np.array_equal(outs[-1], outs[LAFULL])
+    assert_close(outs[-1], outs[NOLA], what="lookahead vs generic path")
+
+
+def test_lookahead_shards_bitwise(amd):
+    """A 24-channel batch split 7 + 17: every channel changes its stagger phase
+    and its index, and the outputs stay bit-identical."""
+    rng = np.random.default_rng(330)
+    C, B, L = 24, 256, 30 * 256
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    one = amd.FFTConvolver.init(hs, B, L, channels=C)
+    a = amd.FFTConvolver.init(hs[:7], B, L, channels=7)
+    b = amd.FFTConvolver.init(hs[7:], B, L, channels=17)
+    assert one.lookahead_parts() > 0
+    for j in range(90):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        y = one.process(x)
+        assert np.array_equal(y, np.concatenate([a.process(x[:7]), b.process(x[7:])])), j
+
+
+def test_lookahead_nan_block(amd, oracle_mod):
+    """A non-finite block in one channel while its neighbours run from windows:
+    zero output, block kept in the input buffer, then recovery -- as the
+    oracle."""
+    rng = np.random.default_rng(340)
+    C, B, L = 4, 256, 40 * 256
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    refs = _refs(oracle_mod, hs, B, L)
+    for j in range(70):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        if j in (45, 46):
+            x[2, 17] = np.nan
+        got = conv.process(x)
+        for c in range(C):
+            r = refs[c].process(x[c])
+            assert np.array_equal(np.isnan(got[c]), np.isnan(r)), (j, c)
+            m = ~np.isnan(r)
+            assert_close(got[c][m], r[m], what=f"block {j} ch {c}")
+            assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
+
+
+def test_lookahead_clone_mid_window(amd):
+    """A clone taken mid-window continues bit-identically (windows copied)."""
+    rng = np.random.default_rng(350)
+    C, B, L = 9, 256, 35 * 256
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    for _ in range(43):
+        conv.process(np.stack([white(rng, B) for _ in range(C)]))
+    twin = conv.clone()
+    for j in range(30):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        assert np.array_equal(conv.process(x), twin.process(x)), j
+
+
+def test_lookahead_device_steps(amd, oracle_mod):
+    """process_device_steps over the lookahead path equals host calls and the
+    oracle (a few sampled channels)."""
+    import torch
+
+    rng = np.random.default_rng(360)
+    C, B, L, K = 64, 256, 48 * 256, 120
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    x = np.stack([white(rng, K * B) for _ in range(C)])
+    dev = torch.device("cuda:0")
+    xd = torch.from_numpy(np.ascontiguousarray(x.reshape(C, K, B).transpose(1, 0, 2))).to(dev)  # [K][C][B]
+    yd = torch.empty_like(xd)
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    s = torch.cuda.Stream(dev)
+    conv.process_device_steps(xd.data_ptr(), B, C * B, yd.data_ptr(), B, C * B, B, K, s.cuda_stream)
+    s.synchronize()
+    y = yd.cpu().numpy().transpose(1, 0, 2).reshape(C, K * B)
+    host = amd.FFTConvolver.init(hs, B, L, channels=C)
+    yh = np.concatenate([host.process(x[:, k * B:(k + 1) * B]) for k in range(K)], axis=1)
+    assert np.array_equal(y, yh)
+    for c in (0, 13, 63):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        assert_close(y[c], np.concatenate([ref.process(x[c, k * B:(k + 1) * B]) for k in range(K)]),
+                     what=f"channel {c}")
