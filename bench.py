@@ -5,7 +5,9 @@ Workload (BASELINE.json configs[1], the north-star metric's config): 1024
 channels per GPU, block 256, a distinct 48,000-tap white-noise IR per channel,
 f32.  One *step* = one FFTConvolver::process call of 256 samples on every
 channel (src/fft_convolver.rs:229-309) = one fused kernel launch: forward R2C
-of the new block into the FDL, the S-segment spectral MAC, C2R and overlap-add.
+of the new block into the FDL, the S-segment spectral MAC, C2R and overlap-add
+-- with the lookahead step (csrc/la.hpp) the far FDL rows' MAC is summed 8
+blocks ahead by the launch's anchor workgroups (C/8 channels per launch).
 Inputs are resident in HBM when the timed region starts.
 
 Multi-GPU (BASELINE configs[3], 8192 channels on 8 GPUs): one process per GPU,
@@ -42,6 +44,25 @@ def algorithmic_bytes_per_channel_block(B: int, L: int) -> int:
     S = -(-L // B)
     K = B + 1
     return 16 * S * K + 8 * K + 4 * B + 4 * B + 8 * B
+
+
+LA_D = 8  # lookahead window (fft-convolution_amd/csrc/la.hpp)
+
+
+def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
+    """Compulsory HBM bytes per channel-block of the lookahead step (la.hpp),
+    in the same units as SURVEY.md §8(d) (K = B+1 bins of 8 B per row):
+    an anchor every D = 8 blocks reads the far H rows [D+1, S) and the FDL
+    ages [1, S-2] once: 8K (2S - D - 3) / D; it writes `parts` partial rows
+    per window step and the step reads them back: 16K parts; plus the new X
+    row (8K), in (4B), out (4B) and overlap r/w (8B).  The near rows (H[1..D]
+    and the last D blocks, 2 x 8K x D per block) are re-read every block from
+    the Infinity Cache by design and are not counted -- the rocprof FETCH_SIZE
+    traffic checks that.  cfg2 (parts 4): 116,405 B."""
+    S = -(-L // B)
+    K = B + 1
+    far = 8 * K * (2 * S - LA_D - 3) // LA_D
+    return far + 16 * K * parts + 8 * K + 4 * B + 4 * B + 8 * B
 
 
 def parse():
@@ -84,7 +105,7 @@ def pmc_traffic(args):
     vals = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir="/tmp")
-        cmd = [prof, "--pmc", counter, "--kernel-include-regex", "upols_process_kernel", "-d", d, "-o", "pmc",
+        cmd = [prof, "--pmc", counter, "--kernel-include-regex", "upols_", "-d", d, "-o", "pmc",
                "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--pmc-inner",
                "--pmc", "off", "--no-cpu-baseline", "--steps", "20", "--warmup", "3",
                "--channels", str(args.channels), "--block", str(args.block), "--ir", str(args.ir)]
@@ -96,7 +117,7 @@ def pmc_traffic(args):
         got = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if r.get("Counter_Name") == counter and "upols_process_kernel" in r.get("Kernel_Name", ""):
+                if r.get("Counter_Name") == counter and "upols_" in r.get("Kernel_Name", ""):
                     got.append(float(r["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not got:
@@ -242,7 +263,15 @@ def main():
     total_samples = args.gpus * C * B * args.steps
     value = total_samples / elapsed / 1e6
     per_launch_s = kern_ms / 1000.0 / args.steps
-    bytes_per_launch = algorithmic_bytes_per_channel_block(B, L) * C
+    canonical_bytes = algorithmic_bytes_per_channel_block(B, L) * C
+    parts = conv.lookahead_parts()
+    if parts:
+        bytes_per_launch = lookahead_bytes_per_channel_block(B, L, parts) * C
+        kname = (f"upols_la_kernel (lookahead step: {C} step workgroups + {C}/{LA_D} x {parts} anchor "
+                 "workgroups per launch)")
+    else:
+        bytes_per_launch = canonical_bytes
+        kname = "upols_process_kernel (fused UPOLS step, one workgroup per channel)"
     achieved = bytes_per_launch / per_launch_s / 1e9
 
     if rank == 0 and args.pmc_inner:
@@ -284,9 +313,13 @@ def main():
                 "traffic": traffic,
                 "traffic_note": traffic_note,
                 "traffic_gbs": round(traffic / per_launch_s / 1e9, 1) if traffic else None,
-                "kernel": "upols_process_kernel (fused UPOLS step, one workgroup per channel)",
+                "kernel": kname,
                 "bytes_per_launch": bytes_per_launch,
                 "launch_us": round(per_launch_s * 1e6, 3),
+                # the reference's algorithm (every block streams all S rows of H
+                # and the FDL) would need this many bytes per launch:
+                "canonical_bytes_per_launch": canonical_bytes,
+                "canonical_equiv_gbs": round(canonical_bytes / per_launch_s / 1e9, 1),
             },
             "cpu_baseline": cpu,
         }

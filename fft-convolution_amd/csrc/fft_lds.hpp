@@ -62,7 +62,8 @@ __device__ __forceinline__ void stage_sync() {
 // Input in buf0; returns the buffer that holds the naturally ordered result
 // (buf0 or buf1).  INV = unnormalised inverse (conjugate twiddles).
 // `tw` is the W_N table with N = 2M.  Every thread of the block must call it
-// (WAVE: a single wave -- NT = 64 -- calls it, synchronising at wave level).
+// (WAVE: a single wave -- NT = 64, any wave of the block -- calls it,
+// synchronising at wave level).
 template <int LOG2M, int NT, bool INV, bool WAVE = false>
 __device__ __forceinline__ float2 *lds_cfft(float2 *buf0, float2 *buf1, const float2 *__restrict__ tw) {
     constexpr int M = 1 << LOG2M;
@@ -70,7 +71,7 @@ __device__ __forceinline__ float2 *lds_cfft(float2 *buf0, float2 *buf1, const fl
     constexpr int R4 = LOG2M / 2;
     float2 *src = buf0;
     float2 *dst = buf1;
-    const int tid = threadIdx.x;
+    const int tid = WAVE ? (int)(threadIdx.x & (NT - 1)) : (int)threadIdx.x;  // WAVE: any one wave
 #pragma unroll
     for (int s = 0; s < R4; ++s) {
         const int Ns = 1 << (2 * s);        // sub-transform length so far

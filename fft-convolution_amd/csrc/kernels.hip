@@ -16,6 +16,7 @@
 // loads (float4 = 2 bins per lane).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -273,7 +274,8 @@ typedef __attribute__((address_space(3))) void *lptr_t;
 template <int NT>
 __device__ __forceinline__ void dma_f32(float *dst, const float *src, int count) {  // any alignment
     const int lane = threadIdx.x & 63;
-    for (int base = (threadIdx.x >> 6) * 64; base < count; base += NT)
+    // NT threads copy: the caller's wave w of them starts at w (NT = 64: any single wave)
+    for (int base = ((threadIdx.x >> 6) % (NT / 64)) * 64; base < count; base += NT)
         if (base + lane < count)
             __builtin_amdgcn_global_load_lds((gptr_t)(src + base + lane), (lptr_t)(dst + base), 4, 0, 0);
 }
@@ -282,7 +284,7 @@ __device__ __forceinline__ void dma_16b(void *dst, const void *src, int bytes) {
     const int lane = threadIdx.x & 63;
     const char *s = static_cast<const char *>(src);
     char *d = static_cast<char *>(dst);
-    for (int base = (threadIdx.x >> 6) * 1024; base < bytes; base += NT * 16)
+    for (int base = ((threadIdx.x >> 6) % (NT / 64)) * 1024; base < bytes; base += NT * 16)
         if (base + lane * 16 < bytes)
             __builtin_amdgcn_global_load_lds((gptr_t)(s + base + lane * 16), (lptr_t)(d + base), 16, 0, 0);
 }
@@ -1220,7 +1222,20 @@ int la_parts(int log2b, int S) {
     if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NOLA)) return 0;
     if (S < 3 * (LA_D + 1)) return 0;
     const int lpw = LA_NT / ((1 << log2b) / 2);
+    // (tuning experiments: FFTCONV_LA_PARTS overrides the parts per channel)
+    if (const char *e = getenv("FFTCONV_LA_PARTS")) {
+        const int w = atoi(e);
+        if (w >= 1 && w * lpw <= LA_NG) return w;
+    }
     return LA_NG / lpw;
+}
+static int la_probe() {  // timing experiments only: FFTCONV_LA_TIMING_PROBE (results are wrong)
+    static const int v = [] { const char *e = getenv("FFTCONV_LA_TIMING_PROBE"); return e ? atoi(e) : 0; }();
+    return v;
+}
+static int la_steps_first() {
+    static const int v = [] { const char *e = getenv("FFTCONV_LA_STEPS_FIRST"); return e ? atoi(e) : 0; }();
+    return v;
 }
 int la_window() { return LA_D; }
 
@@ -1230,9 +1245,11 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         return hipErrorNotSupported;
     } else {
         using LG = LaGeo<LOG2B>;
+        using LS = LaStep<LOG2B>;
         constexpr size_t gen = Geo<LOG2B, LA_NT>::lds_bytes;
-        constexpr size_t lds0 = LG::step_bytes > LG::anchor_bytes ? LG::step_bytes : LG::anchor_bytes;
-        constexpr size_t lds = lds0 > gen ? lds0 : gen;
+        constexpr size_t lds0 = LS::bytes > LG::anchor_bytes ? LS::bytes : LG::anchor_bytes;
+        constexpr size_t lds1 = lds0 > gen ? lds0 : gen;
+        constexpr size_t lds = (lds1 + 15) / 16 * 16;
         if (a.la_W * LG::LPW > LA_NG || a.la_W < 1) return hipErrorInvalidValue;
         // the far-row streams: nontemporal once the whole H + FDL working set
         // (re-read every D steps) exceeds the Infinity Cache
@@ -1242,6 +1259,9 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         ProcArgs args = a;
         args.pipe = 0;
         args.lag = 0;
+        args.la_channels = channels;
+        args.la_steps_first = la_steps_first();
+        args.la_probe = la_probe();
         if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) {
             args.la_all = -1;  // no anchors: every eligible step sums all its rows
             args.la_nanchor = 0;
@@ -1250,7 +1270,8 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(kern, dim3(args.la_nanchor + channels), dim3(LA_NT), lds, s, args);
+        const int nstep = (channels + LS::NCH - 1) / LS::NCH;
+        hipLaunchKernelGGL(kern, dim3(args.la_nanchor + nstep), dim3(LA_NT), lds, s, args);
         return hipGetLastError();
     }
 }

@@ -92,6 +92,9 @@ struct ProcArgs {
     int la_all;            // 1: every channel is scheduled for an anchor (entry launch); -1: none is
     int la_t;              // launch counter mod LA_D: channel c anchors when (c - t) % LA_D == 0
     int la_seq;            // 1 or 2, alternating per lookahead launch; 0 in every other launch
+    int la_steps_first;    // grid order: step workgroups before the anchors (tuning)
+    int la_probe;          // timing probe only (wrong results): 1 = anchors idle, 2 = steps idle
+    int la_channels;       // channels of the batch (step workgroups cover LaStep::NCH each)
 };
 
 struct IrArgs {

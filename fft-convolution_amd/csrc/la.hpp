@@ -181,9 +181,6 @@ __device__ __forceinline__ void la_chain(LaAcc &acc, const RowStream &hs, const 
 template <int LOG2B>
 struct LaGeo {
     static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;
-    // step role: bufA | bufB | tw (2B) | H0 | pre (float2) | overlap | tail0 | tail1 (float) | pad | groups
-    static constexpr size_t step_front = 6 * 8 * (size_t)B + 3 * 4 * (size_t)B + 16;
-    static constexpr size_t step_bytes = step_front + (size_t)LA_NG * F * 16;
     static constexpr size_t anchor_bytes = (size_t)(LPW - 1) * LA_D * F * 16;
 };
 
@@ -260,71 +257,131 @@ __device__ __forceinline__ void la_anchor(const ProcArgs &a, int b, unsigned cha
 }
 
 // ---------------------------------------------------------------------------
-// Step workgroup: one full block of channel c (FFTConvolver::process
-// :229-309 for the common call).  Wave 0 runs the transform chain (R2C of the
-// block into FDL row `current`, then conv, C2R, overlap-add) while waves 1-3
-// form pre = near rows D..1 + far partials (from the window, or -- `full` --
-// from the far-row groups all four waves computed first).
+// Step workgroup: one full block of each of NCH channels (FFTConvolver::
+// process :229-309 for the common call).  Wave k < NCH runs channel k's
+// transform chain (R2C of the block into FDL row `current`, then conv, C2R,
+// overlap-add) while the other waves form every channel's
+// pre = near rows D..1 + far partials (from the window, or -- `full` -- from
+// the far-row groups all four waves sum first).  Two channels per workgroup
+// at B <= 256: the step and anchor workgroups of a launch then fit the CUs
+// together (4 workgroups per CU at 128 VGPRs), so the anchors' stream runs
+// under the steps' transform chains instead of after them.
 // ---------------------------------------------------------------------------
-template <int LOG2B, bool NTL>
-__device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, size_t c, int4 st, bool full,
-                                        bool sched, unsigned char *smem) {
-    using LG = LaGeo<LOG2B>;
-    constexpr int B = LG::B, F = LG::F, LPW = LG::LPW;
+template <int LOG2B>
+struct LaStep {
+    static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;
+    static constexpr int NCH = LOG2B <= 8 ? 2 : 1;           // channels per step workgroup
+    static constexpr int HL = LA_NT - 64 * NCH;               // helper lanes
+    static constexpr int TPL = (NCH * F + HL - 1) / HL;       // pre slots per helper lane
+    // tw (2B float2) | per channel: bufA | bufB | H0 | pre (float2) | overlap | tail0 | tail1 (float)
+    static constexpr size_t ch_bytes = 4 * 8 * (size_t)B + 3 * 4 * (size_t)B;
+    static constexpr size_t chain_bytes = 16 * (size_t)B + NCH * ch_bytes;
+    // the full pass's group partials alias the chain buffers (done before them)
+    static constexpr size_t grp_bytes = (size_t)NCH * LA_NG * F * 16;
+    static constexpr size_t bytes = chain_bytes > grp_bytes ? chain_bytes : grp_bytes;
+};
+
+template <int LOG2B, bool NTL, int NCH>
+__device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, const int (&cs)[NCH],
+                                        const int4 (&st)[NCH], const bool (&full)[NCH], const bool (&sched)[NCH],
+                                        int nvalid, unsigned char *smem) {
+    using LS = LaStep<LOG2B>;
+    constexpr int B = LS::B, F = LS::F, LPW = LS::LPW;
+    constexpr int HL = LA_NT - 64 * NCH;
+    constexpr int TPL = (NCH * F + HL - 1) / HL;
     constexpr int ROWB = B * (int)sizeof(float2);
     constexpr float invN = 1.0f / (float)(2 * B);
-    float2 *bufA = reinterpret_cast<float2 *>(smem);
-    float2 *bufB = bufA + B;
-    float2 *twl = bufB + B;
-    float2 *h0l = twl + 2 * B;
-    float2 *prel = h0l + B;
-    float *ovl = reinterpret_cast<float *>(prel + B);
-    float *p0l = ovl + B;
-    float *p1l = p0l + B;
-    float4 *grp = reinterpret_cast<float4 *>(smem + LG::step_front);  // [NG][F]
+    constexpr size_t chb = 4 * 8 * (size_t)B + 3 * 4 * (size_t)B;
+    float2 *twl = reinterpret_cast<float2 *>(smem);
+    auto chan_lds = [&](int k) { return smem + 16 * (size_t)B + (size_t)k * chb; };
+    float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][NG][F], full pass only
 
-    const int cur = __builtin_amdgcn_readfirstlane(st.x), act = __builtin_amdgcn_readfirstlane(st.y);
-    const int flags = __builtin_amdgcn_readfirstlane(st.w);
+    static_assert(NCH == 1 || NCH == 2, "one or two channels per step workgroup");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W = a.la_W, NG = W * LPW;
+    // per-channel values by a runtime channel index without private-array
+    // indexing (which would put the arrays in scratch)
+    auto ST = [&](int k) { return (NCH == 1 || k == 0) ? st[0] : st[NCH - 1]; };
+    auto CS = [&](int k) { return (NCH == 1 || k == 0) ? cs[0] : cs[NCH - 1]; };
+    auto FULL = [&](int k) { return (NCH == 1 || k == 0) ? full[0] : full[NCH - 1]; };
+    auto SCHED = [&](int k) { return (NCH == 1 || k == 0) ? sched[0] : sched[NCH - 1]; };
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
-    const float2 *Hc = J.H + c * rows;
-    float2 *Xc = J.X + c * rows;
-    float *ovc = J.overlap + c * B;
-    float *outc = J.out + c * J.out_stride;
-    const float *inc = J.in + c * J.in_stride;
-    const int curp = cur > 0 ? cur - 1 : act - 1;  // current after this block (:301-305)
-    const RowStream hs(Hc, bytes), xs(Xc, bytes);
+    bool anyfull = false;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) anyfull |= k < nvalid && FULL(k);
 
-    if (full) {
-        // every far-row group's chain for this step, into LDS
+    // helper slot t of this lane: channel k, slot f (valid if k < nvalid)
+    auto task = [&](int t, int &k, int &f) {
+        const int idx = (tid - 64 * NCH) + t * HL;
+        k = idx / F;
+        f = idx - k * F;
+        return idx < NCH * F && k < nvalid;
+    };
+    float4 Areg[TPL];
+    if (anyfull) {
+        // every far-row group's chain of the channels that sum everything, into LDS
         const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
-        for (int g = l; g < NG; g += LPW) {
-            int lo, hi;
-            la_group(g, NG, act, lo, hi);
-            LaAcc acc;
-            acc.zero();
-            if (g & 1) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
-            else la_chain<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
-            grp[g * F + f] = acc.get();
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            if (k >= nvalid || !FULL(k)) continue;
+            const int cur = __builtin_amdgcn_readfirstlane(ST(k).x), act = __builtin_amdgcn_readfirstlane(ST(k).y);
+            const RowStream hs(J.H + (size_t)CS(k) * rows, bytes), xs(J.X + (size_t)CS(k) * rows, bytes);
+            for (int g = l; g < NG; g += LPW) {
+                int lo, hi;
+                la_group(g, NG, act, lo, hi);
+                LaAcc acc;
+                acc.zero();
+                if (g & 1) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+                else la_chain<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+                grp[(k * NG + g) * F + f] = acc.get();
+            }
         }
         __syncthreads();
+        if (wave >= NCH) {  // each helper slot's A, in the anchors' tree order
+#pragma unroll
+            for (int t = 0; t < TPL; ++t) {
+                int k, f;
+                if (!task(t, k, f) || !FULL(k)) continue;
+                float4 A;
+                for (int w = 0; w < W; ++w) {
+                    float4 pw = grp[(k * NG + w * LPW) * F + f];
+#pragma unroll
+                    for (int q = 1; q < LPW; ++q) pw = vadd(pw, grp[(k * NG + w * LPW + q) * F + f]);
+                    A = w == 0 ? pw : vadd(A, pw);
+                }
+                Areg[t] = A;
+            }
+        }
+        __syncthreads();  // the chain buffers below overwrite the group partials
     }
 
     float2 *Z = nullptr, *Q = nullptr;
-    if (wave == 0) {
-        // ---- transform chain, one wave: the block -> R2C -> FDL row `current`
+    if (wave < NCH) {
+        if (wave >= nvalid) return;
+        // ---- transform chain of channel k = wave: the block -> R2C -> FDL row `current`
+        const int k = wave;
+        const size_t c = (size_t)CS(k);
+        const int cur = __builtin_amdgcn_readfirstlane(ST(k).x);
+        float2 *bufA = reinterpret_cast<float2 *>(chan_lds(k));
+        float2 *bufB = bufA + B, *h0l = bufB + B;
+        float *ovl = reinterpret_cast<float *>(h0l + 2 * B);
+        float *p0l = ovl + B, *p1l = p0l + B;
+        const float *inc = J.in + c * J.in_stride;
         dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);  // x[0..B) as packed z[0..B/2)
         for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
-        dma_16b<64>(twl, a.tw, 2 * B * (int)sizeof(float2));
-        dma_16b<64>(h0l, Hc, B * (int)sizeof(float2));
-        dma_f32<64>(ovl, ovc, B);
+        if (k == 0) dma_16b<64>(twl, a.tw, 2 * B * (int)sizeof(float2));
+        dma_16b<64>(h0l, J.H + c * rows, B * (int)sizeof(float2));
+        dma_f32<64>(ovl, J.overlap + c * B, B);
         if (J.add0) dma_f32<64>(p0l, J.add0 + c * J.add_stride, B);
         if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wave_sync();
+        if constexpr (NCH > 1) {
+            __syncthreads();  // wave 0's twiddle table is in LDS
+        } else {
+            wave_sync();
+        }
         if (J.tin) {  // two-stage: append the block to tail_input (:473-475)
             const float *xb = reinterpret_cast<const float *>(bufA);
             float *ti = J.tin + c * J.tin_stride;
@@ -333,17 +390,22 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, siz
         wave_sync();
         Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :243-255
         Q = Z == bufA ? bufB : bufA;
-        float2 *Xcur = Xc + (size_t)cur * B;
+        float2 *Xcur = J.X + c * rows + (size_t)cur * B;
         for (int m = lane; m < B; m += 64) {
             const float2 v = real_post<LOG2B, 64>(Z, m, twl);
             Q[m] = v;
             Xcur[m] = v;
         }
     } else {
+        if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
         // ---- pre = near chain (rows D..1) + far partials A, canonical order
-        const int wj = la_jget(flags);
-        const int win = (flags & FLAG_PWIN) ? 1 : 0;
-        for (int f = tid - 64; f < F; f += LA_NT - 64) {
+#pragma unroll
+        for (int t = 0; t < TPL; ++t) {
+            int k, f;
+            if (!task(t, k, f)) continue;
+            const size_t c = (size_t)CS(k);
+            const int cur = ST(k).x, act = ST(k).y, flags = ST(k).w;
+            const RowStream hs(J.H + c * rows, bytes), xs(J.X + c * rows, bytes);
             float4 hv[LA_D], xv[LA_D];
 #pragma unroll
             for (int i = LA_D; i >= 1; --i) {
@@ -353,15 +415,11 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, siz
                 xv[i - 1] = xs.ld4<false>(f * 16, r * ROWB);
             }
             float4 A;
-            if (full) {
-                for (int w = 0; w < W; ++w) {
-                    float4 pw = grp[(w * LPW) * F + f];
-#pragma unroll
-                    for (int q = 1; q < LPW; ++q) pw = vadd(pw, grp[(w * LPW + q) * F + f]);
-                    A = w == 0 ? pw : vadd(A, pw);
-                }
+            if (FULL(k)) {
+                A = Areg[t];
             } else {
-                const float4 *P0 = la_prow(a, c, win, wj, 0, B);
+                const int win = (flags & FLAG_PWIN) ? 1 : 0;
+                const float4 *P0 = la_prow(a, c, win, la_jget(flags), 0, B);
                 A = P0[f];
                 for (int w = 1; w < W; ++w) A = vadd(A, P0[(size_t)w * F + f]);
             }
@@ -369,12 +427,24 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, siz
             acc.zero();
 #pragma unroll
             for (int i = LA_D; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
+            float2 *prel = reinterpret_cast<float2 *>(chan_lds(k)) + 3 * B;
             reinterpret_cast<float4 *>(prel)[f] = vadd(acc.get(), A);
+            __builtin_amdgcn_sched_barrier(0);  // one slot's 2D + W rows in flight at a time
         }
     }
     __syncthreads();
-    if (wave != 0) return;
+    if (wave >= NCH) return;
 
+    const int k = wave;
+    const size_t c = (size_t)CS(k);
+    const int cur = __builtin_amdgcn_readfirstlane(ST(k).x), act = __builtin_amdgcn_readfirstlane(ST(k).y);
+    const int flags = __builtin_amdgcn_readfirstlane(ST(k).w);
+    float2 *bufA = reinterpret_cast<float2 *>(chan_lds(k));
+    float2 *h0l = bufA + 2 * B, *prel = bufA + 3 * B;
+    float *ovl = reinterpret_cast<float *>(bufA + 4 * B);
+    float *p0l = ovl + B, *p1l = p0l + B;
+    float *outc = J.out + c * J.out_stride;
+    float *ovc = J.overlap + c * B;
     bool bad = false;  // conv = pre + X (.) H[0] (:270-275), then the C2R error check
     for (int f = lane; f < F; f += 64) {
         const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
@@ -400,14 +470,16 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, siz
             ovc[j] = y[B + j] * invN;  // :297-298
         }
         if (lane == 0) {
+            const int curp = cur > 0 ? cur - 1 : act - 1;  // :301-305
             int nf = (keep ^ FLAG_REV) | tag;
-            if (sched) nf = (nf ^ FLAG_PWIN) | FLAG_LA | (la_dnew((int)c, a) << LA_D_SHIFT);
-            else if (!full) nf |= FLAG_LA | ((la_jget(flags) + 1) << LA_J_SHIFT) | (la_dget(flags) << LA_D_SHIFT);
+            if (SCHED(k)) nf = (nf ^ FLAG_PWIN) | FLAG_LA | (la_dnew((int)c, a) << LA_D_SHIFT);
+            else if (!FULL(k)) nf |= FLAG_LA | ((la_jget(flags) + 1) << LA_J_SHIFT) | (la_dget(flags) << LA_D_SHIFT);
             J.state[c] = make_int4(curp, act, 0, nf);
         }
     } else {
         // output.fill(0); return (:278-281): the block stays in the input
         // buffer, fill / current unchanged; the window is dropped
+        const float *inc = J.in + c * J.in_stride;
         float *ibc = J.inbuf + c * B;
         for (int j = lane; j < B; j += 64) {
             float v = 0.f;
@@ -422,23 +494,61 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, siz
     }
 }
 
+// a channel off the lookahead path (partial block, buffered input, short
+// response) in the workgroup: its channels run one at a time, out of line
+// (the rare fallback keeps its registers out of the step's allocation)
 template <int LOG2B, bool NTL>
-__global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int b = blockIdx.x;
-    if (b < a.la_nanchor) {
-        la_anchor<LOG2B, NTL>(a, b, smem);
-        return;
-    }
-
-    const size_t c = (size_t)(b - a.la_nanchor);
+__device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0, int nvalid, unsigned char *smem) {
+    const ProcArgs &a = *ap;
     const ProcJob &J = a.job[0];
-    const int4 st = J.state[c];
-    if (la_eligible<LOG2B>(st, J.n)) {
-        const bool usable = (st.w & FLAG_LA) && la_jget(st.w) < la_dget(st.w);
-        la_step<LOG2B, NTL>(a, J, c, st, !usable, la_sched((int)c, a), smem);
-    } else {
-        process_job<LOG2B, LA_NT, false, NTL>(a, J, c, st, smem);
+    for (int k = 0; k < nvalid; ++k) {
+        if (k) __syncthreads();
+        const int c = c0 + k;
+        const int4 st = J.state[c];
+        if (la_eligible<LOG2B>(st, J.n)) {
+            const int c1[1] = {c};
+            const int4 s1[1] = {st};
+            const bool f1[1] = {!((st.w & FLAG_LA) && la_jget(st.w) < la_dget(st.w))};
+            const bool h1[1] = {la_sched(c, a)};
+            la_step<LOG2B, NTL, 1>(a, J, c1, s1, f1, h1, 1, smem);
+        } else {
+            process_job<LOG2B, LA_NT, false, NTL>(a, J, (size_t)c, st, smem);
+        }
     }
 }
 
+template <int LOG2B, bool NTL>
+__global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
+    using LS = LaStep<LOG2B>;
+    constexpr int NCH = LS::NCH;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int nstep = (int)gridDim.x - a.la_nanchor;  // step workgroups
+    const int b = blockIdx.x;
+    const int ba = a.la_steps_first ? b - nstep : b;  // anchor index, < 0 for a step
+    if (ba >= 0 && ba < a.la_nanchor) {
+        if (a.la_probe != 1) la_anchor<LOG2B, NTL>(a, ba, smem);
+        return;
+    }
+    if (a.la_probe == 2) return;
+    const int c0 = (a.la_steps_first ? b : b - a.la_nanchor) * NCH;
+    const ProcJob &J = a.job[0];
+    const int nvalid = min(NCH, a.la_channels - c0);
+    int cs[NCH];
+    int4 st[NCH];
+    bool full[NCH], sched[NCH];
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+        cs[k] = c0 + k;
+        int4 v = k < nvalid ? J.state[cs[k]] : make_int4(0, 0, 0, 0);
+        // wave-uniform: keep the state words in scalar registers
+        st[k] = make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                          __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+        all &= k >= nvalid || la_eligible<LOG2B>(st[k], J.n);
+        full[k] = !((st[k].w & FLAG_LA) && la_jget(st[k].w) < la_dget(st[k].w));
+        sched[k] = la_sched(cs[k], a);
+    }
+    if (all) la_step<LOG2B, NTL, NCH>(a, J, cs, st, full, sched, nvalid, smem);
+    else  // (the arguments by their kernarg address: no private copy of the block)
+        la_fallback<LOG2B, NTL>((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), c0, nvalid, smem);
+}
