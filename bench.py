@@ -6,8 +6,9 @@ channels per GPU, block 256, a distinct 48,000-tap white-noise IR per channel,
 f32.  One *step* = one FFTConvolver::process call of 256 samples on every
 channel (src/fft_convolver.rs:229-309) = one fused kernel launch: forward R2C
 of the new block into the FDL, the S-segment spectral MAC, C2R and overlap-add
--- with the lookahead step (csrc/la.hpp) the far FDL rows' MAC is summed 8
-blocks ahead by the launch's anchor workgroups (C/8 channels per launch).
+-- with the lookahead step (csrc/la.hpp) the FDL rows beyond the 4 nearest are
+summed ahead by the launch's anchor workgroups (rows 5..16 four blocks ahead
+for C/4 channels, rows >= 17 sixteen blocks ahead for C/16 channels).
 Inputs are resident in HBM when the timed region starts.
 
 Multi-GPU (BASELINE configs[3], 8192 channels on 8 GPUs): one process per GPU,
@@ -46,23 +47,27 @@ def algorithmic_bytes_per_channel_block(B: int, L: int) -> int:
     return 16 * S * K + 8 * K + 4 * B + 4 * B + 8 * B
 
 
-LA_D = 8  # lookahead window (fft-convolution_amd/csrc/la.hpp)
+LA_D1, LA_DM, LA_DF = 4, 4, 16  # lookahead levels (fft-convolution_amd/csrc/la.hpp)
 
 
 def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
-    """Compulsory HBM bytes per channel-block of the lookahead step (la.hpp),
-    in the same units as SURVEY.md §8(d) (K = B+1 bins of 8 B per row):
-    an anchor every D = 8 blocks reads the far H rows [D+1, S) and the FDL
-    ages [1, S-2] once: 8K (2S - D - 3) / D; it writes `parts` partial rows
-    per window step and the step reads them back: 16K parts; plus the new X
-    row (8K), in (4B), out (4B) and overlap r/w (8B).  The near rows (H[1..D]
-    and the last D blocks, 2 x 8K x D per block) are re-read every block from
-    the Infinity Cache by design and are not counted -- the rocprof FETCH_SIZE
-    traffic checks that.  cfg2 (parts 4): 116,405 B."""
+    """Bytes per channel-block the lookahead step (la.hpp) reads and writes, in
+    the units of SURVEY.md §8(d) (rows of K = B+1 bins, 8 B per bin):
+      far anchor every DF blocks: far H rows [DF+1, S) and FDL ages [1, S-2]
+        once: 8K (2S - DF - 3) / DF;
+      mid anchor every DM blocks: H rows [D1+1, DF] and ages [1, DF-1]:
+        8K (2 DF - D1 - 1) / DM;
+      near rows (step): H[1..D1] and the last D1 blocks: 8K * 2 D1;
+      window rows written by the anchors and read by the steps: 16K (parts + 1);
+      the new X row, H[0], in, out, overlap r/w: 16K + 16B.
+    cfg2 (parts 2): 96,744 B, against 779,208 B for the reference's
+    algorithm (every block streams all S rows of H and of the FDL)."""
     S = -(-L // B)
     K = B + 1
-    far = 8 * K * (2 * S - LA_D - 3) // LA_D
-    return far + 16 * K * parts + 8 * K + 4 * B + 4 * B + 8 * B
+    far = 8 * K * (2 * S - LA_DF - 3) // LA_DF
+    mid = 8 * K * (2 * LA_DF - LA_D1 - 1) // LA_DM
+    near = 8 * K * 2 * LA_D1
+    return far + mid + near + 16 * K * (parts + 1) + 16 * K + 16 * B
 
 
 def parse():
@@ -267,8 +272,8 @@ def main():
     parts = conv.lookahead_parts()
     if parts:
         bytes_per_launch = lookahead_bytes_per_channel_block(B, L, parts) * C
-        kname = (f"upols_la_kernel (lookahead step: {C} step workgroups + {C}/{LA_D} x {parts} anchor "
-                 "workgroups per launch)")
+        kname = (f"upols_la_kernel (lookahead step: step workgroups of 2 channels + far anchors for "
+                 f"{C}/{LA_DF} and mid anchors for {C}/{LA_DM} channels per launch)")
     else:
         bytes_per_launch = canonical_bytes
         kname = "upols_process_kernel (fused UPOLS step, one workgroup per channel)"

@@ -137,8 +137,8 @@ struct UniformCore {
     Scratch scratch;
     // lookahead (la.hpp): standalone batches only (la_ok, set before init)
     bool la_ok = false;
-    int la_W = 0;                 // anchor workgroups per channel, 0 = off
-    DevPtr<float2> laP;           // [C][2][LA_D][la_W][B] far-row windows
+    int la_W = 0;                 // far parts (partial rows per step), 0 = off
+    DevPtr<float2> laP, laPm;     // far [C][2][DF][la_W][B] / mid [C][2][DM][B] windows
     unsigned long long la_t = 0;  // lookahead launches so far (stagger clock)
     int la_seq = 1;               // launch tag, alternating 1 / 2
     bool la_all = true;           // next lookahead launch re-anchors every channel
@@ -173,7 +173,9 @@ struct UniformCore {
         if (int r = staging.alloc(C * ir_len)) return r;  // update() never allocates
         la_W = la_ok ? la_parts(log2b, (int)S) : 0;
         if (la_W) {
-            if (int r = laP.alloc(C * 2 * (size_t)la_window() * (size_t)la_W * B)) return r;
+            const LaDims d = la_dims(log2b);
+            if (int r = laP.alloc(C * 2 * (size_t)d.DF * (size_t)la_W * B)) return r;
+            if (int r = laPm.alloc(C * 2 * (size_t)d.DM * B)) return r;
         }
         // twiddles W_N^k in double, rounded to f32
         std::vector<float2> t(2 * B);
@@ -289,17 +291,23 @@ struct UniformCore {
         a.tw = tw.p;
         a.njobs = 1;
         if (la_W && n == B && la_parts(log2b, (int)S) == la_W) {
-            // lookahead launch: C step workgroups behind this launch's anchors
-            // (every channel on entry, else the stagger class (c - t) % D == 0)
-            const size_t D = (size_t)la_window();
-            const size_t t0 = (size_t)(la_t % D);
-            const size_t nch = la_all ? C : (C > t0 ? (C - t0 + D - 1) / D : 0);
+            // lookahead launch: the step workgroups behind this launch's far
+            // and mid anchors (every channel on entry, else the stagger
+            // classes (c - t) % period == 0)
+            const LaDims d = la_dims(log2b);
+            auto count = [&](size_t P) {
+                const size_t t0 = (size_t)(la_t % P);
+                return la_all ? C : (C > t0 ? (C - t0 + P - 1) / P : 0);
+            };
             a.laP = laP.p;
+            a.laPm = laPm.p;
             a.la_W = la_W;
             a.la_all = la_all ? 1 : 0;
-            a.la_t = (int)t0;
+            a.la_t = (int)(la_t % (unsigned long long)d.DF);
             a.la_seq = la_seq;
-            a.la_nanchor = (int)(nch * (size_t)la_W);
+            // (far anchors: whole rounds of 8 channels, one XCD each -- see la_anchor_far)
+            a.la_nfar = (int)((count((size_t)d.DF) + 7) / 8 * 8 * (size_t)d.wg_far);
+            a.la_nmid = (int)count((size_t)d.DM);
             HIP_TRY(launch_process_la(log2b, a, (int)C, s));
             ++la_t;
             la_seq = 3 - la_seq;
@@ -345,6 +353,7 @@ struct UniformCore {
         if (int r = cp(inbuf, o.inbuf)) return r;
         if (int r = cp(state, o.state)) return r;
         if (int r = cp(laP, o.laP)) return r;
+        if (int r = cp(laPm, o.laPm)) return r;
         la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
         if (int r = staging.alloc(o.staging.n)) return r;
         HIP_TRY(hipStreamSynchronize(stream));

@@ -116,15 +116,38 @@ __device__ __forceinline__ bool slot0_finite(float2 v) { return isfinite(v.x) &&
 // aux 2 = nontemporal.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// FFTCONV_DEBUG_BOUNDS (debug builds only): report out-of-range stream rows
+// and window/state indices with printf instead of touching the memory
+#ifdef FFTCONV_DEBUG_BOUNDS
+#define DBG_CHECK(cond, ...)                                                   \
+    do {                                                                       \
+        if (!(cond)) printf("BOUNDS " __VA_ARGS__);                            \
+    } while (0)
+#else
+#define DBG_CHECK(cond, ...) do {} while (0)
+#endif
 struct RowStream {
     __amdgpu_buffer_rsrc_t r;
+#ifdef FFTCONV_DEBUG_BOUNDS
+    int nbytes;
+#endif
     __device__ __forceinline__ RowStream(const float2 *base, size_t bytes) {
         r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2 *>(base), 0, (int)bytes, 0x00020000);
+#ifdef FFTCONV_DEBUG_BOUNDS
+        nbytes = (int)bytes;
+#endif
     }
     // (an explicitly typed vector + memcpy: indexing the builtin's result
     // through __builtin_bit_cast made hipcc emit a single-dword load)
     template <bool NTL>
     __device__ __forceinline__ float4 ld4(int voff, int soff) const {
+#ifdef FFTCONV_DEBUG_BOUNDS
+        if (voff < nbytes && (soff < 0 || soff + voff + 16 > nbytes)) {
+            printf("BOUNDS ld4 blk %d tid %d voff %d soff %d nbytes %d\n", (int)blockIdx.x, (int)threadIdx.x, voff,
+                   soff, nbytes);
+            soff = 0;
+        }
+#endif
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, NTL ? 2 : 0);
         float4 f;
         __builtin_memcpy(&f, &v, sizeof(f));
@@ -1190,6 +1213,13 @@ static hipError_t launch_ir_t(const IrArgs &a, int channels, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifdef FFTCONV_DEBUG_BOUNDS  // (debug builds: block 256 only, to keep the compile short)
+#define FFTCONV_DISPATCH(FN, LOG2B, ...)                      \
+    switch (LOG2B) {                                          \
+        case 8: return FN<8>(__VA_ARGS__);                    \
+        default: return hipErrorNotSupported;                 \
+    }
+#else
 #define FFTCONV_DISPATCH(FN, LOG2B, ...)                      \
     switch (LOG2B) {                                          \
         case 0: return FN<0>(__VA_ARGS__);                    \
@@ -1208,6 +1238,7 @@ static hipError_t launch_ir_t(const IrArgs &a, int channels, hipStream_t s) {
         case 13: return FN<13>(__VA_ARGS__);                  \
         default: return hipErrorInvalidValue;                 \
     }
+#endif
 
 hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;
@@ -1220,14 +1251,16 @@ hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_
 int la_parts(int log2b, int S) {
     if (log2b < 7 || log2b > 9) return 0;
     if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NOLA)) return 0;
-    if (S < 3 * (LA_D + 1)) return 0;
-    const int lpw = LA_NT / ((1 << log2b) / 2);
-    // (tuning experiments: FFTCONV_LA_PARTS overrides the parts per channel)
-    if (const char *e = getenv("FFTCONV_LA_PARTS")) {
-        const int w = atoi(e);
-        if (w >= 1 && w * lpw <= LA_NG) return w;
+    if (S < 2 * LA_DF) return 0;
+    switch (log2b) {
+        case 7: return LaGeo<7>::WF;
+        case 8: return LaGeo<8>::WF;
+        default: return LaGeo<9>::WF;
     }
-    return LA_NG / lpw;
+}
+LaDims la_dims(int log2b) {
+    const int wg = log2b == 7 ? LaGeo<7>::WG_FAR : (log2b == 8 ? LaGeo<8>::WG_FAR : LaGeo<9>::WG_FAR);
+    return LaDims{LA_DF, LA_DM, wg};
 }
 static int la_probe() {  // timing experiments only: FFTCONV_LA_TIMING_PROBE (results are wrong)
     static const int v = [] { const char *e = getenv("FFTCONV_LA_TIMING_PROBE"); return e ? atoi(e) : 0; }();
@@ -1237,7 +1270,6 @@ static int la_steps_first() {
     static const int v = [] { const char *e = getenv("FFTCONV_LA_STEPS_FIRST"); return e ? atoi(e) : 0; }();
     return v;
 }
-int la_window() { return LA_D; }
 
 template <int LOG2B>
 static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
@@ -1250,7 +1282,7 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         constexpr size_t lds0 = LS::bytes > LG::anchor_bytes ? LS::bytes : LG::anchor_bytes;
         constexpr size_t lds1 = lds0 > gen ? lds0 : gen;
         constexpr size_t lds = (lds1 + 15) / 16 * 16;
-        if (a.la_W * LG::LPW > LA_NG || a.la_W < 1) return hipErrorInvalidValue;
+        if (a.la_W != LG::WF || !a.laPm) return hipErrorInvalidValue;
         // the far-row streams: nontemporal once the whole H + FDL working set
         // (re-read every D steps) exceeds the Infinity Cache
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
@@ -1264,14 +1296,14 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         args.la_probe = la_probe();
         if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) {
             args.la_all = -1;  // no anchors: every eligible step sums all its rows
-            args.la_nanchor = 0;
+            args.la_nfar = args.la_nmid = 0;
         }
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
         const int nstep = (channels + LS::NCH - 1) / LS::NCH;
-        hipLaunchKernelGGL(kern, dim3(args.la_nanchor + nstep), dim3(LA_NT), lds, s, args);
+        hipLaunchKernelGGL(kern, dim3(args.la_nfar + args.la_nmid + nstep), dim3(LA_NT), lds, s, args);
         return hipGetLastError();
     }
 }

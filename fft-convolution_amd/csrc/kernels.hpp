@@ -10,16 +10,21 @@ enum : int {
     FLAG_REV = 2,    // scan parity of the segment MAC (toggled per completed block)
     FLAG_PRE = 4,    // pre[] holds pre_multiplied of the block that starts at `current`
     FLAG_XSYNC = 8,  // crossfade pair: this FDL has always equalled its partner's
-    // lookahead (time-blocked FDL, see la.hpp): an anchor's window of far-row
-    // partial sums is live (FLAG_LA) in P window FLAG_PWIN; bits 8-11 = steps of
-    // the window consumed, 12-15 = window length; bits 16-17 = the launch
-    // sequence tag of the last process launch that wrote this state word
+    // lookahead (time-blocked FDL, see la.hpp): the far window of partial
+    // sums is live (FLAG_LA) in P window FLAG_PWIN, bits 8-11 = steps of it
+    // consumed, 12-15 = its length - 1; the mid window likewise (FLAG_LAM,
+    // FLAG_PWINM, bits 18-19, 20-21); bits 16-17 = the launch tag of the last
+    // process launch that wrote this state word
     FLAG_LA = 16,
     FLAG_PWIN = 32,
+    FLAG_LAM = 64,
+    FLAG_PWINM = 128,
     LA_J_SHIFT = 8,
     LA_D_SHIFT = 12,
     SEQ_SHIFT = 16,
-    LA_MASK = FLAG_LA | (15 << LA_J_SHIFT) | (15 << LA_D_SHIFT),
+    LA_JM_SHIFT = 18,
+    LA_DM_SHIFT = 20,
+    LA_MASK = FLAG_LA | FLAG_LAM | (15 << LA_J_SHIFT) | (15 << LA_D_SHIFT) | (3 << LA_JM_SHIFT) | (3 << LA_DM_SHIFT),
     SEQ_MASK = 3 << SEQ_SHIFT,
 };
 
@@ -86,14 +91,17 @@ struct ProcArgs {
     int fuse_mix;          // crossfade pair launch: mix A and B into mix.out in-kernel
     CrossfadeMixArgs mix;  // (buf_a / buf_b unused then)
     // lookahead launch (launch_process_la; job[0] only)
-    float2 *laP;           // [C][2 windows][LA_D][la_W][B] far-row partial sums
-    int la_W;              // anchor workgroups per channel
-    int la_nanchor;        // anchor workgroups at the front of the grid
-    int la_all;            // 1: every channel is scheduled for an anchor (entry launch); -1: none is
-    int la_t;              // launch counter mod LA_D: channel c anchors when (c - t) % LA_D == 0
+    float2 *laP;           // [C][2 windows][LA_DF][la_W][B] far-row partial sums
+    float2 *laPm;          // [C][2 windows][LA_DM][B] mid-row partial sums
+    int la_W;              // far parts (partial rows per step)
+    int la_nfar;           // far anchor workgroups at the front of the grid
+    int la_nmid;           // mid anchor workgroups after them
+    int la_all;            // 1: every channel is scheduled for anchors (entry launch); -1: none is
+    int la_t;              // launch counter mod LA_DF: channel c anchors at period P when (c - t) % P == 0
     int la_seq;            // 1 or 2, alternating per lookahead launch; 0 in every other launch
     int la_steps_first;    // grid order: step workgroups before the anchors (tuning)
-    int la_probe;          // timing probe only (wrong results): 1 = anchors idle, 2 = steps idle
+    int la_probe;          // timing probe only (wrong results): 1 = anchors idle, 2 = steps idle,
+                           // 3 = far anchors only, 4 = mid anchors only
     int la_channels;       // channels of the batch (step workgroups cover LaStep::NCH each)
 };
 
@@ -138,9 +146,13 @@ bool pair_supported(int log2b, int S);
 hipError_t launch_process_pair(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hipStream_t s);
 size_t process_lds_bytes(int log2b);
-// lookahead: anchor workgroups per channel for this geometry, 0 = not used
+// lookahead: far parts (partial rows per step) for this geometry, 0 = not used
 int la_parts(int log2b, int S);
-int la_window();  // LA_D
+struct LaDims {
+    int DF, DM;     // far / mid periods
+    int wg_far;     // workgroups per far anchor
+};
+LaDims la_dims(int log2b);
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 
 constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)

@@ -1,50 +1,58 @@
 // la.hpp -- lookahead step: FFTConvolver::process with the FDL sum
-// re-associated in time (included by kernels.hip after its helpers).
+// re-associated in time (included by kernels.hip, inside namespace fftconv,
+// after its helpers).
 //
 // The reference computes, for every block s of a channel (src/fft_convolver.rs
 // :258-275),
 //     conv_s = sum_{i=1}^{act-1} H[i] (.) X_{s-i}  +  H[0] (.) X_s
 // where X_b is the spectrum of block b (FDL row (current + age) % act).  Every
-// step re-reads all act rows of H and of the FDL: 16 B per bin-row, the whole
-// 773 KB per channel-block at cfg2.  But a far row i > D only meets blocks
-// that are at least i - D steps old, so the terms of the next D steps that
-// use far rows are known D steps ahead.  An *anchor* at step a computes them
-// all in ONE pass over H and the FDL, keeping a window of D X rows in
-// registers:
-//     P_j = sum_{i > D} H[i] (.) X_{a+j-i},    j = 1..D
-// and the D steps that follow only add their D near rows (H[1..D] and the
-// last D blocks: 32 KB per channel, hot in the Infinity Cache) and H[0] X_s.
-// The far-row bytes per channel-block drop from 16 S B to ~16 S B / D; the
-// per-step work stays zero-latency (step s needs nothing after block s).
+// step re-reads all act rows of H and of the FDL: 16 B per bin-row, 773 KB
+// per channel-block at cfg2.  But a row i only meets blocks at least i steps
+// old, so its terms for the next j < i steps are known now.  The rows split in
+// three levels by that horizon:
+//   near rows  1..D1       summed by each step itself;
+//   mid rows   D1+1..DF    summed by a *mid anchor* every DM = D1 steps, for
+//                          the DM steps after it (X ages >= 1 at the anchor);
+//   far rows   DF+1..act-1 summed by a *far anchor* every DF steps, for the
+//                          DF steps after it.
+// An anchor walks its rows once, keeping a window of X rows in registers, and
+// leaves one partial-sum row per future step (P windows in HBM).  Per channel-
+// block the far rows then cost 16 B (S - DF) / DF per bin instead of 16 B S,
+// the mid rows 16 B (DF - D1) / DM, the near rows 16 B D1 (hot in the
+// Infinity Cache).  The step stays zero-latency: step s needs nothing after
+// block s.
 //
-// Anchors are staggered over channels (channel c anchors when (c - t) % D
-// == 0, t = launch counter), so every launch carries C / D anchors and the
-// per-launch bytes are even.  Anchor and step workgroups of one launch touch
-// disjoint memory: an anchor reads FDL ages >= 1 (the step writes age 0) and
-// writes the other P window (two windows per channel, FLAG_PWIN).
+// Anchors are staggered over channels (channel c anchors at level L when
+// (c - t) % period_L == 0, t = launch counter), so every launch carries C/DF
+// far and C/DM mid anchors and the per-launch bytes are even.  Anchor and step
+// workgroups of one launch touch disjoint memory: an anchor reads FDL ages
+// >= 1 (the step writes age 0) and writes the other P window of its level
+// (two per channel and level).
 //
-// Summation order (canonical, phase independent).  The far rows [D+1, act)
-// split into NG fixed groups; each group is ONE sequential chain over its
-// rows (even groups descending, odd ascending -- neighbouring groups then
-// read their shared window rows at the same time); groups combine in a
-// fixed tree (sequentially within an anchor workgroup's lanesets, then over
-// the workgroups).  The near rows D..1 form their own chain, then
-//     pre = near + A,    conv = pre + H[0] (.) X_s     (slot_mac, as :270-275).
-// An anchor's j-th accumulator visits exactly the rows and the blocks the
-// step a+j would, in the same order, so a step served from a window and a
-// step that computes everything itself (entry, after update / reset /
-// partial calls) produce the same bits.  Results therefore do not depend on
-// the stagger, the channel index or the shard size.
+// Summation order (canonical, phase independent).  Each level is a fixed set
+// of sequential chains: near rows D1..1; mid rows DF..D1+1; far rows [DF+1,
+// act) in NG fixed groups (even groups descending, odd ascending, so that
+// neighbouring groups read their shared window rows at the same time) combined
+// sequentially within a far part and then over the parts.  Then
+//     pre = near + (mid + far),   conv = pre + H[0] (.) X_s   (slot_mac, :270-275).
+// An anchor's accumulator for step a+j visits exactly the rows and blocks the
+// step a+j would, in the same order, so a step served from windows and a step
+// that sums everything itself (entry, after update / reset / partial calls,
+// VARIANT_LAFULL) give the same bits: results do not depend on the stagger,
+// the channel index or the shard size.
 #pragma once
 // (no namespace of its own: included inside namespace fftconv)
 
-constexpr int LA_D = 8;             // steps served per anchor (window)
-constexpr int LA_U = 2;             // anchor: H / X rows in flight per lane
-constexpr int LA_RS = LA_D + LA_U;  // anchor: X register ring (window + prefetch)
-constexpr int LA_NT = 256;          // threads per workgroup (anchor and step roles)
-constexpr int LA_NG = 8;            // far-row groups
-constexpr int LA_CU = 8;            // full-pass chain: rows in flight per lane
-constexpr int LA_OOB = 0x7ffffff0;  // a buffer voffset past every stream's range
+constexpr int LA_D1 = 4;             // near rows, summed by the step
+constexpr int LA_DM = 4;             // mid period / window (<= LA_D1)
+constexpr int LA_DF = 16;            // far period / window; mid rows are D1+1..DF
+constexpr int LA_JW = 8;             // far window steps per laneset (register window)
+constexpr int LA_U = 2;              // anchor: H / X rows in flight per lane
+constexpr int LA_NT = 256;           // threads per workgroup (anchor and step roles)
+constexpr int LA_NG = 4;             // far-row groups
+constexpr int LA_CU = 8;             // full-pass chain: rows in flight per lane
+constexpr int LA_OOB = 0x7ffffff0;   // a buffer voffset past every stream's range
+static_assert(LA_DM <= LA_D1 && LA_DF % LA_JW == 0, "lookahead levels");
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -76,53 +84,76 @@ struct LaAcc {
     __device__ __forceinline__ float4 get() const { return make_float4(a01.x, a01.y, a23.x, a23.y); }
 };
 
-__device__ __forceinline__ int la_jget(int w) { return (w >> LA_J_SHIFT) & 15; }
-__device__ __forceinline__ int la_dget(int w) { return (w >> LA_D_SHIFT) & 15; }
+// state word fields (kernels.hpp): far window {FLAG_LA, FLAG_PWIN, j, d-1},
+// mid window {FLAG_LAM, FLAG_PWINM, jm, dm-1}
+__device__ __forceinline__ int la_jf(int w) { return (w >> LA_J_SHIFT) & 15; }
+__device__ __forceinline__ int la_df(int w) { return ((w >> LA_D_SHIFT) & 15) + 1; }
+__device__ __forceinline__ int la_jm(int w) { return (w >> LA_JM_SHIFT) & 3; }
+__device__ __forceinline__ int la_dm(int w) { return ((w >> LA_DM_SHIFT) & 3) + 1; }
+__device__ __forceinline__ bool la_far_live(int w) { return (w & FLAG_LA) && la_jf(w) < la_df(w); }
+__device__ __forceinline__ bool la_mid_live(int w) { return (w & FLAG_LAM) && la_jm(w) < la_dm(w); }
 
 // the lookahead step applies: one whole block from an empty input buffer, at
 // least one far row
 template <int LOG2B>
 __device__ __forceinline__ bool la_eligible(int4 st, int n) {
-    return n == (1 << LOG2B) && st.z == 0 && !(st.w & FLAG_INBUF) && st.y >= LA_D + 2 && st.x < st.y;
+    return n == (1 << LOG2B) && st.z == 0 && !(st.w & FLAG_INBUF) && st.y >= LA_DF + 2 && st.x < st.y;
 }
-__device__ __forceinline__ int la_phase(int c, const ProcArgs &a) {
-    const int r = (c - a.la_t) % LA_D;
-    return r < 0 ? r + LA_D : r;
+// stagger phase of channel c at level period P (la_t = launch counter mod DF)
+__device__ __forceinline__ int la_phase(int c, const ProcArgs &a, int P) {
+    const int r = (c - a.la_t) % P;
+    return r < 0 ? r + P : r;
 }
-__device__ __forceinline__ bool la_sched(int c, const ProcArgs &a) {
-    return a.la_all > 0 || (a.la_all == 0 && la_phase(c, a) == 0);
+__device__ __forceinline__ bool la_sched(int c, const ProcArgs &a, int P) {
+    return a.la_all > 0 || (a.la_all == 0 && la_phase(c, a, P) == 0);
 }
 // window of a new anchor: up to the channel's next stagger slot
-__device__ __forceinline__ int la_dnew(int c, const ProcArgs &a) {
-    const int r = la_phase(c, a);
-    return r == 0 ? LA_D : r;
+__device__ __forceinline__ int la_dnew(int c, const ProcArgs &a, int P) {
+    const int r = la_phase(c, a, P);
+    return r == 0 ? P : r;
 }
-// far-row group g of NG: rows [lo, hi) of [D+1, act)
-__device__ __forceinline__ void la_group(int g, int NG, int act, int &lo, int &hi) {
-    const int nf = act - LA_D - 1;
-    lo = LA_D + 1 + (g * nf) / NG;
-    hi = LA_D + 1 + ((g + 1) * nf) / NG;
+// far-row group g of NG: rows [lo, hi) of [DF+1, act)
+__device__ __forceinline__ void la_group(int g, int act, int &lo, int &hi) {
+    const int nf = act - LA_DF - 1;
+    lo = LA_DF + 1 + (g * nf) / LA_NG;
+    hi = LA_DF + 1 + ((g + 1) * nf) / LA_NG;
 }
-// P row of (channel, window, step j of the window, anchor part w)
-__device__ __forceinline__ float4 *la_prow(const ProcArgs &a, size_t c, int win, int j, int w, int B) {
-    return reinterpret_cast<float4 *>(a.laP + ((((c * 2 + win) * LA_D + j) * (size_t)a.la_W + w) * (size_t)B));
+// window rows: far P[c][win][j][w] (w < la_W parts), mid P[c][win][j]
+__device__ __forceinline__ float4 *la_pf(const ProcArgs &a, size_t c, int win, int j, int w, int B) {
+#ifdef FFTCONV_DEBUG_BOUNDS
+    if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && j >= 0 && j < LA_DF && w >= 0 && w < a.la_W)) {
+        printf("BOUNDS la_pf blk %d c %d win %d j %d w %d\n", (int)blockIdx.x, (int)c, win, j, w);
+        c = 0; win = 0; j = 0; w = 0;
+    }
+#endif
+    return reinterpret_cast<float4 *>(a.laP + ((((c * 2 + win) * LA_DF + j) * (size_t)a.la_W + w) * (size_t)B));
+}
+__device__ __forceinline__ float4 *la_pm(const ProcArgs &a, size_t c, int win, int j, int B) {
+#ifdef FFTCONV_DEBUG_BOUNDS
+    if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && j >= 0 && j < LA_DM)) {
+        printf("BOUNDS la_pm blk %d c %d win %d j %d\n", (int)blockIdx.x, (int)c, win, j);
+        c = 0; win = 0; j = 0;
+    }
+#endif
+    return reinterpret_cast<float4 *>(a.laPm + (((c * 2 + win) * LA_DM + j) * (size_t)B));
 }
 
 // ---------------------------------------------------------------------------
-// Anchor walk over one far-row group [lo, hi) in direction ASC: for window
-// steps j = 1..D, acc[j-1] += H[i] (.) X(age i - j at the anchor), rows in
-// the group's order.  X rows live in a register ring indexed by the walk
-// position e (age lo - D + e ascending, hi - 2 - e descending); each row of H
-// and of the FDL is loaded once, LA_U rows ahead.
+// Anchor walk over rows [lo, hi) in direction ASC for window steps
+// j = j0+1 .. j0+JW: acc[jj] += H[i] (.) X(age i - j0 - 1 - jj at the anchor),
+// rows in the chain's order.  X rows live in a register ring indexed by the
+// walk position e; each row of H and of the FDL is loaded once, LA_U ahead.
 // ---------------------------------------------------------------------------
-template <int LOG2B, bool ASC, bool NTL>
-__device__ __forceinline__ void la_walk(LaAcc (&acc)[LA_D], const RowStream &hs, const RowStream &xs, int voff,
-                                        bool z0, int lo, int hi, int cur, int act) {
+template <int LOG2B, bool ASC, bool NTL, int JW>
+__device__ __forceinline__ void la_walk(LaAcc (&acc)[JW], const RowStream &hs, const RowStream &xs, int voff,
+                                        bool z0, int lo, int hi, int j0, int cur, int act) {
     constexpr int ROWB = (1 << LOG2B) * (int)sizeof(float2);
+    constexpr int RS = JW + LA_U;                         // X ring: window + prefetch
+    constexpr int UNR = RS % LA_U == 0 ? RS : RS * LA_U;  // static ring slots
     const int n = hi - lo;
-    const int ne = n + LA_D - 1;
+    const int ne = n + JW - 1;
     auto xoff = [&](int e) {
-        const int age = ASC ? lo - LA_D + e : hi - 2 - e;
+        const int age = ASC ? lo - j0 - JW + e : hi - 2 - j0 - e;
         int r = cur + age;
         if (r >= act) r -= act;
         return r * ROWB;
@@ -131,22 +162,23 @@ __device__ __forceinline__ void la_walk(LaAcc (&acc)[LA_D], const RowStream &hs,
     // rows past the walk are loaded from an out-of-range buffer offset (zero,
     // no memory access): no branches around the loads, no register copies
     auto vo = [&](bool in) { return in ? voff : LA_OOB; };
-    float4 xr[LA_RS], hr[LA_U];
+    float4 xr[RS], hr[LA_U];
 #pragma unroll
-    for (int e = 0; e < LA_RS - 1; ++e) xr[e] = xs.ld4<NTL>(vo(e < ne), xoff(e < ne ? e : 0));
+    for (int e = 0; e < RS - 1; ++e) xr[e] = xs.ld4<NTL>(vo(e < ne), xoff(e < ne ? e : 0));
 #pragma unroll
     for (int k = 0; k < LA_U; ++k) hr[k] = hs.ld4<NTL>(vo(k < n), hoff(k < n ? k : 0));
-    for (int k0 = 0; k0 < n; k0 += LA_RS) {
+#pragma nounroll
+    for (int k0 = 0; k0 < n; k0 += UNR) {  // (not unrolled: a constant walk would hoist every load)
 #pragma unroll
-        for (int u = 0; u < LA_RS; ++u) {
+        for (int u = 0; u < UNR; ++u) {
             const int k = k0 + u;
             if (k >= n) break;
             const LaH h = la_ops(hr[u % LA_U], z0);
 #pragma unroll
-            for (int j = 0; j < LA_D; ++j) acc[j].mac(h, xr[(ASC ? u + LA_D - 1 - j : u + j) % LA_RS]);
-            const bool hin = k + LA_U < n, xin = k + LA_RS - 1 < ne;
+            for (int jj = 0; jj < JW; ++jj) acc[jj].mac(h, xr[(ASC ? u + JW - 1 - jj : u + jj) % RS]);
+            const bool hin = k + LA_U < n, xin = k + RS - 1 < ne;
             hr[u % LA_U] = hs.ld4<NTL>(vo(hin), hoff(hin ? k + LA_U : 0));
-            xr[(u + LA_RS - 1) % LA_RS] = xs.ld4<NTL>(vo(xin), xoff(xin ? k + LA_RS - 1 : 0));
+            xr[(u + RS - 1) % RS] = xs.ld4<NTL>(vo(xin), xoff(xin ? k + RS - 1 : 0));
             // keep the issue order: the scheduler would otherwise hoist the
             // loads of later rows and run out of registers
             __builtin_amdgcn_sched_barrier(0);
@@ -154,13 +186,14 @@ __device__ __forceinline__ void la_walk(LaAcc (&acc)[LA_D], const RowStream &hs,
     }
 }
 
-// One group's chain for the current step (window step 0: X age i), the same
-// rows in the same order as an anchor's accumulators.
+// One chain for the current step (X age i), the same rows in the same order
+// as an anchor's accumulators.
 template <int LOG2B, bool ASC, bool NTL>
 __device__ __forceinline__ void la_chain(LaAcc &acc, const RowStream &hs, const RowStream &xs, int voff, bool z0,
                                          int lo, int hi, int cur, int act) {
     constexpr int ROWB = (1 << LOG2B) * (int)sizeof(float2);
     const int n = hi - lo;
+#pragma nounroll
     for (int k0 = 0; k0 < n; k0 += LA_CU) {
         float4 hv[LA_CU], xv[LA_CU];
 #pragma unroll
@@ -180,80 +213,131 @@ __device__ __forceinline__ void la_chain(LaAcc &acc, const RowStream &hs, const 
 
 template <int LOG2B>
 struct LaGeo {
-    static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;
-    static constexpr size_t anchor_bytes = (size_t)(LPW - 1) * LA_D * F * 16;
+    static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;  // lanesets of F lanes per workgroup
+    // far anchor workgroup: GPW groups (one per laneset) of one window half;
+    // one anchor = WF parts x (DF / JW) halves, XCD-aligned (see la_anchor_far)
+    static constexpr int GPW = LPW < LA_NG ? LPW : LA_NG;
+    static constexpr int WF = LA_NG / GPW;                          // far parts (P rows per step)
+    static constexpr int WG_FAR = WF * (LA_DF / LA_JW);             // workgroups per far anchor
+    static constexpr int JM = LA_DM / (LPW > LA_DM ? LA_DM : LPW);  // mid window steps per laneset
+    static constexpr size_t anchor_bytes = (size_t)(GPW - 1) * LA_JW * F * 16;
 };
 
-// ---------------------------------------------------------------------------
-// Anchor workgroup b: part w of channel c's anchor (groups w*LPW .. +LPW-1,
-// one per laneset of F lanes), combined in laneset order and stored as
-// window rows P[win][j][w], j < d.
-// ---------------------------------------------------------------------------
-template <int LOG2B, bool NTL>
-__device__ __forceinline__ void la_anchor(const ProcArgs &a, int b, unsigned char *smem) {
-    using LG = LaGeo<LOG2B>;
-    constexpr int B = LG::B, F = LG::F, LPW = LG::LPW;
+// the anchor's view of channel c: its ring position, window and length, or
+// false if this launch opens no window of the level (period P) at c
+template <int LOG2B>
+__device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int c, int P, int &cur, int &act, int &win,
+                                                int &d) {
     const ProcJob &J = a.job[0];
-    const int W = a.la_W;
-    const int ci = b / W, w = b - ci * W;
-    const int c = a.la_all > 0 ? ci : a.la_t + LA_D * ci;
+    DBG_CHECK(c >= 0 && c < a.la_channels, "anchor state blk %d c %d P %d\n", (int)blockIdx.x, c, P);
     const int4 st = J.state[c];
     const int sx = __builtin_amdgcn_readfirstlane(st.x), sy = __builtin_amdgcn_readfirstlane(st.y);
     const int sz = __builtin_amdgcn_readfirstlane(st.z), sw = __builtin_amdgcn_readfirstlane(st.w);
-    const int act = sy;
-    int cur, win, d;
+    const bool far = P == LA_DF;
+    act = sy;
     if (((sw & SEQ_MASK) >> SEQ_SHIFT) == a.la_seq) {
         // this launch's step has already stored the channel's state: it
         // opened a window iff the state says so (j = 0)
-        if (!(sw & FLAG_LA) || la_jget(sw) != 0) return;
+        if (far ? (!(sw & FLAG_LA) || la_jf(sw) != 0) : (!(sw & FLAG_LAM) || la_jm(sw) != 0)) return false;
         cur = sx + 1 == act ? 0 : sx + 1;
-        win = (sw & FLAG_PWIN) ? 1 : 0;
-        d = la_dget(sw);
+        win = (sw & (far ? FLAG_PWIN : FLAG_PWINM)) ? 1 : 0;
+        d = far ? la_df(sw) : la_dm(sw);
     } else {
-        if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return;
+        if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return false;
         cur = sx;
-        win = (sw & FLAG_PWIN) ? 0 : 1;
-        d = la_dnew(c, a);
+        win = (sw & (far ? FLAG_PWIN : FLAG_PWINM)) ? 0 : 1;
+        d = la_dnew(c, a, P);
     }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Far anchor workgroup b: part w, window half(s) of channel c's far anchor
+// (groups w*GPW .. +GPW-1), combined in group order and stored as window rows
+// Pf[win][j][w].
+// ---------------------------------------------------------------------------
+template <int LOG2B, bool NTL>
+__device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned char *smem) {
+    using LG = LaGeo<LOG2B>;
+    constexpr int B = LG::B, F = LG::F, GPW = LG::GPW;
+    const ProcJob &J = a.job[0];
+    // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so the
+    // WG_FAR workgroups of one anchor sit 8 apart -- on one XCD, whose L2
+    // then serves the rows the window halves and neighbouring groups share
+    const int x = b & 7, y = b >> 3;
+    const int ci = (y / LG::WG_FAR) * 8 + x, r = y % LG::WG_FAR;
+    const int c = a.la_all > 0 ? ci : a.la_t + LA_DF * ci;
+    if (c >= a.la_channels) return;  // (padding of the last XCD round)
+    int cur, act, win, d;
+    if (!la_anchor_state<LOG2B>(a, c, LA_DF, cur, act, win, d)) return;
 
     const int tid = threadIdx.x;
     const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
-    const int NG = W * LPW, g = w * LPW + l;
+    if (l >= GPW) return;                              // (more lanesets than groups)
+    const int w = r % LG::WF;                          // part
+    const int h = r / LG::WF;                          // window half: steps h*JW+1 .. h*JW+JW
+    const int g = w * GPW + l;
     int lo, hi;
-    la_group(g, NG, act, lo, hi);
+    la_group(g, act, lo, hi);
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
     const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
-    LaAcc acc[LA_D];
+    LaAcc acc[LA_JW];
 #pragma unroll
-    for (int j = 0; j < LA_D; ++j) acc[j].zero();
+    for (int j = 0; j < LA_JW; ++j) acc[j].zero();
     if (hi > lo) {
-        if (g & 1) la_walk<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
-        else la_walk<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+        if (g & 1) la_walk<LOG2B, true, NTL, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        else la_walk<LOG2B, false, NTL, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
     }
-    if constexpr (LPW > 1) {
-        float4 *red = reinterpret_cast<float4 *>(smem);  // [LPW-1][D][F]
+    if constexpr (GPW > 1) {
+        float4 *red = reinterpret_cast<float4 *>(smem);  // [GPW-1][JW][F]
         if (l > 0) {
 #pragma unroll
-            for (int j = 0; j < LA_D; ++j) red[((l - 1) * LA_D + j) * F + f] = acc[j].get();
+            for (int j = 0; j < LA_JW; ++j) red[((l - 1) * LA_JW + j) * F + f] = acc[j].get();
         }
         __syncthreads();
         if (l == 0) {
 #pragma unroll
-            for (int j = 0; j < LA_D; ++j) {
-                if (j < d) {
+            for (int j = 0; j < LA_JW; ++j) {
+                if (h * LA_JW + j < d) {
                     float4 p = acc[j].get();
 #pragma unroll
-                    for (int q = 1; q < LPW; ++q) p = vadd(p, red[((q - 1) * LA_D + j) * F + f]);
-                    la_prow(a, c, win, j, w, B)[f] = p;
+                    for (int q = 1; q < GPW; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * F + f]);
+                    la_pf(a, c, win, h * LA_JW + j, w, B)[f] = p;
                 }
             }
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < LA_D; ++j)
-            if (j < d) la_prow(a, c, win, j, w, B)[f] = acc[j].get();
+        for (int j = 0; j < LA_JW; ++j)
+            if (h * LA_JW + j < d) la_pf(a, c, win, h * LA_JW + j, w, B)[f] = acc[j].get();
     }
+}
+
+// Mid anchor workgroup b: channel c's mid rows DF..D1+1 (one descending chain
+// per window step), the window steps split over the lanesets.
+template <int LOG2B, bool NTL>
+__device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
+    using LG = LaGeo<LOG2B>;
+    constexpr int B = LG::B, F = LG::F, JM = LG::JM;
+    const ProcJob &J = a.job[0];
+    const int c = a.la_all > 0 ? b : (a.la_t % LA_DM) + LA_DM * b;
+    if (c >= a.la_channels) return;
+    int cur, act, win, d;
+    if (!la_anchor_state<LOG2B>(a, c, LA_DM, cur, act, win, d)) return;
+    const int tid = threadIdx.x;
+    const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
+    if (l * JM >= LA_DM) return;  // (more lanesets than window steps)
+    const size_t rows = (size_t)J.S * B;
+    const size_t bytes = rows * sizeof(float2);
+    const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
+    LaAcc acc[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) acc[j].zero();
+    la_walk<LOG2B, false, false, JM>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, l * JM, cur, act);
+#pragma unroll
+    for (int j = 0; j < JM; ++j)
+        if (l * JM + j < d) la_pm(a, c, win, l * JM + j, B)[f] = acc[j].get();
 }
 
 // ---------------------------------------------------------------------------
@@ -261,56 +345,55 @@ __device__ __forceinline__ void la_anchor(const ProcArgs &a, int b, unsigned cha
 // process :229-309 for the common call).  Wave k < NCH runs channel k's
 // transform chain (R2C of the block into FDL row `current`, then conv, C2R,
 // overlap-add) while the other waves form every channel's
-// pre = near rows D..1 + far partials (from the window, or -- `full` -- from
-// the far-row groups all four waves sum first).  Two channels per workgroup
-// at B <= 256: the step and anchor workgroups of a launch then fit the CUs
-// together (4 workgroups per CU at 128 VGPRs), so the anchors' stream runs
-// under the steps' transform chains instead of after them.
+// pre = near + (mid + far), the mid / far partials from their windows or --
+// when a level has no live window (entry, after update / reset / partial
+// calls) -- from chains all four waves sum first.  Two channels per
+// workgroup at B <= 256: the step and anchor workgroups of a launch then fit
+// the CUs together, so the anchors' stream runs under the transform chains.
 // ---------------------------------------------------------------------------
 template <int LOG2B>
 struct LaStep {
     static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;
     static constexpr int NCH = LOG2B <= 8 ? 2 : 1;           // channels per step workgroup
-    static constexpr int HL = LA_NT - 64 * NCH;               // helper lanes
-    static constexpr int TPL = (NCH * F + HL - 1) / HL;       // pre slots per helper lane
     // tw (2B float2) | per channel: bufA | bufB | H0 | pre (float2) | overlap | tail0 | tail1 (float)
     static constexpr size_t ch_bytes = 4 * 8 * (size_t)B + 3 * 4 * (size_t)B;
     static constexpr size_t chain_bytes = 16 * (size_t)B + NCH * ch_bytes;
-    // the full pass's group partials alias the chain buffers (done before them)
-    static constexpr size_t grp_bytes = (size_t)NCH * LA_NG * F * 16;
+    // the full pass's chain results (mid + NG far groups per channel) alias
+    // the chain buffers (they are consumed before the chains start)
+    static constexpr size_t grp_bytes = (size_t)NCH * (1 + LA_NG) * F * 16;
     static constexpr size_t bytes = chain_bytes > grp_bytes ? chain_bytes : grp_bytes;
 };
 
 template <int LOG2B, bool NTL, int NCH>
 __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, const int (&cs)[NCH],
-                                        const int4 (&st)[NCH], const bool (&full)[NCH], const bool (&sched)[NCH],
-                                        int nvalid, unsigned char *smem) {
+                                        const int4 (&st)[NCH], int nvalid, unsigned char *smem) {
     using LS = LaStep<LOG2B>;
-    constexpr int B = LS::B, F = LS::F, LPW = LS::LPW;
+    using LG = LaGeo<LOG2B>;
+    constexpr int B = LS::B, F = LS::F, LPW = LS::LPW, GPW = LG::GPW, WF = LG::WF;
     constexpr int HL = LA_NT - 64 * NCH;
     constexpr int TPL = (NCH * F + HL - 1) / HL;
+    constexpr int NCHAIN = 1 + LA_NG;  // full pass: mid chain + far groups, per channel
     constexpr int ROWB = B * (int)sizeof(float2);
     constexpr float invN = 1.0f / (float)(2 * B);
-    constexpr size_t chb = 4 * 8 * (size_t)B + 3 * 4 * (size_t)B;
+    constexpr size_t chb = LS::ch_bytes;
+    static_assert(NCH == 1 || NCH == 2, "one or two channels per step workgroup");
     float2 *twl = reinterpret_cast<float2 *>(smem);
     auto chan_lds = [&](int k) { return smem + 16 * (size_t)B + (size_t)k * chb; };
-    float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][NG][F], full pass only
+    float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][NCHAIN][F], full pass only
 
-    static_assert(NCH == 1 || NCH == 2, "one or two channels per step workgroup");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int W = a.la_W, NG = W * LPW;
+    const size_t rows = (size_t)J.S * B;
+    const size_t bytes = rows * sizeof(float2);
     // per-channel values by a runtime channel index without private-array
     // indexing (which would put the arrays in scratch)
     auto ST = [&](int k) { return (NCH == 1 || k == 0) ? st[0] : st[NCH - 1]; };
     auto CS = [&](int k) { return (NCH == 1 || k == 0) ? cs[0] : cs[NCH - 1]; };
-    auto FULL = [&](int k) { return (NCH == 1 || k == 0) ? full[0] : full[NCH - 1]; };
-    auto SCHED = [&](int k) { return (NCH == 1 || k == 0) ? sched[0] : sched[NCH - 1]; };
-    const size_t rows = (size_t)J.S * B;
-    const size_t bytes = rows * sizeof(float2);
+    auto fullF = [&](int k) { return !la_far_live(ST(k).w); };
+    auto fullM = [&](int k) { return !la_mid_live(ST(k).w); };
     bool anyfull = false;
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) anyfull |= k < nvalid && FULL(k);
+    for (int k = 0; k < NCH; ++k) anyfull |= k < nvalid && (fullF(k) || fullM(k));
 
     // helper slot t of this lane: channel k, slot f (valid if k < nvalid)
     auto task = [&](int t, int &k, int &f) {
@@ -319,51 +402,68 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         f = idx - k * F;
         return idx < NCH * F && k < nvalid;
     };
-    float4 Areg[TPL];
+    float4 Mreg[TPL], Freg[TPL];
+#pragma unroll
+    for (int t = 0; t < TPL; ++t) Mreg[t] = Freg[t] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (anyfull) {
-        // every far-row group's chain of the channels that sum everything, into LDS
+        // the chains of the levels without a live window, into LDS
         const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
 #pragma unroll
         for (int k = 0; k < NCH; ++k) {
-            if (k >= nvalid || !FULL(k)) continue;
+            if (k >= nvalid) continue;
             const int cur = __builtin_amdgcn_readfirstlane(ST(k).x), act = __builtin_amdgcn_readfirstlane(ST(k).y);
+            const bool fm = fullM(k), ff = fullF(k);
             const RowStream hs(J.H + (size_t)CS(k) * rows, bytes), xs(J.X + (size_t)CS(k) * rows, bytes);
-            for (int g = l; g < NG; g += LPW) {
+            for (int q = l; q < NCHAIN; q += LPW) {
+                if (q == 0 ? !fm : !ff) continue;
                 int lo, hi;
-                la_group(g, NG, act, lo, hi);
+                if (q == 0) {
+                    lo = LA_D1 + 1;
+                    hi = LA_DF + 1;
+                } else {
+                    la_group(q - 1, act, lo, hi);
+                }
                 LaAcc acc;
                 acc.zero();
-                if (g & 1) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+                if (q > 0 && ((q - 1) & 1)) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
                 else la_chain<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
-                grp[(k * NG + g) * F + f] = acc.get();
+                grp[(k * NCHAIN + q) * F + f] = acc.get();
             }
         }
         __syncthreads();
-        if (wave >= NCH) {  // each helper slot's A, in the anchors' tree order
+        if (wave >= NCH) {  // each helper slot's mid chain and far tree (the anchors' order)
 #pragma unroll
             for (int t = 0; t < TPL; ++t) {
                 int k, f;
-                if (!task(t, k, f) || !FULL(k)) continue;
-                float4 A;
-                for (int w = 0; w < W; ++w) {
-                    float4 pw = grp[(k * NG + w * LPW) * F + f];
+                if (!task(t, k, f)) continue;
+                if (fullM(k)) Mreg[t] = grp[(k * NCHAIN) * F + f];
+                if (fullF(k)) {
+                    float4 A;
 #pragma unroll
-                    for (int q = 1; q < LPW; ++q) pw = vadd(pw, grp[(k * NG + w * LPW + q) * F + f]);
-                    A = w == 0 ? pw : vadd(A, pw);
+                    for (int w = 0; w < WF; ++w) {
+                        float4 pw = grp[(k * NCHAIN + 1 + w * GPW) * F + f];
+#pragma unroll
+                        for (int qq = 1; qq < GPW; ++qq) pw = vadd(pw, grp[(k * NCHAIN + 1 + w * GPW + qq) * F + f]);
+                        A = w == 0 ? pw : vadd(A, pw);
+                    }
+                    Freg[t] = A;
                 }
-                Areg[t] = A;
             }
         }
-        __syncthreads();  // the chain buffers below overwrite the group partials
+        __syncthreads();  // the chain buffers below overwrite the chain results
     }
 
-    float2 *Z = nullptr, *Q = nullptr;
-    if (wave < NCH) {
-        if (wave >= nvalid) return;
+    float2 *Z = reinterpret_cast<float2 *>(chan_lds(0)), *Q = Z + B;
+    if (wave < NCH && wave >= nvalid) {
+        // (no channel for this chain wave: it still takes part in the barriers)
+        if constexpr (NCH > 1) __syncthreads();
+    } else if (wave < NCH) {
         // ---- transform chain of channel k = wave: the block -> R2C -> FDL row `current`
         const int k = wave;
         const size_t c = (size_t)CS(k);
         const int cur = __builtin_amdgcn_readfirstlane(ST(k).x);
+        DBG_CHECK(c < (size_t)a.la_channels && cur >= 0 && cur < J.S, "step chain blk %d c %d cur %d nvalid %d\n",
+                  (int)blockIdx.x, (int)c, cur, nvalid);
         float2 *bufA = reinterpret_cast<float2 *>(chan_lds(k));
         float2 *bufB = bufA + B, *h0l = bufB + B;
         float *ovl = reinterpret_cast<float *>(h0l + 2 * B);
@@ -398,7 +498,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         }
     } else {
         if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
-        // ---- pre = near chain (rows D..1) + far partials A, canonical order
+        // ---- pre = near chain (rows D1..1) + (mid + far), canonical order
 #pragma unroll
         for (int t = 0; t < TPL; ++t) {
             int k, f;
@@ -406,34 +506,39 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             const size_t c = (size_t)CS(k);
             const int cur = ST(k).x, act = ST(k).y, flags = ST(k).w;
             const RowStream hs(J.H + c * rows, bytes), xs(J.X + c * rows, bytes);
-            float4 hv[LA_D], xv[LA_D];
+            float4 hv[LA_D1], xv[LA_D1];
 #pragma unroll
-            for (int i = LA_D; i >= 1; --i) {
+            for (int i = LA_D1; i >= 1; --i) {
                 int r = cur + i;
                 if (r >= act) r -= act;
                 hv[i - 1] = hs.ld4<false>(f * 16, i * ROWB);
                 xv[i - 1] = xs.ld4<false>(f * 16, r * ROWB);
             }
-            float4 A;
-            if (FULL(k)) {
-                A = Areg[t];
+            float4 M, A;
+            if (fullM(k)) {
+                M = Mreg[t];
             } else {
-                const int win = (flags & FLAG_PWIN) ? 1 : 0;
-                const float4 *P0 = la_prow(a, c, win, la_jget(flags), 0, B);
+                M = la_pm(a, c, (flags & FLAG_PWINM) ? 1 : 0, la_jm(flags), B)[f];
+            }
+            if (fullF(k)) {
+                A = Freg[t];
+            } else {
+                const float4 *P0 = la_pf(a, c, (flags & FLAG_PWIN) ? 1 : 0, la_jf(flags), 0, B);
                 A = P0[f];
-                for (int w = 1; w < W; ++w) A = vadd(A, P0[(size_t)w * F + f]);
+#pragma unroll
+                for (int w = 1; w < WF; ++w) A = vadd(A, P0[(size_t)w * F + f]);
             }
             LaAcc acc;
             acc.zero();
 #pragma unroll
-            for (int i = LA_D; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
+            for (int i = LA_D1; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
             float2 *prel = reinterpret_cast<float2 *>(chan_lds(k)) + 3 * B;
-            reinterpret_cast<float4 *>(prel)[f] = vadd(acc.get(), A);
-            __builtin_amdgcn_sched_barrier(0);  // one slot's 2D + W rows in flight at a time
+            reinterpret_cast<float4 *>(prel)[f] = vadd(acc.get(), vadd(M, A));
+            __builtin_amdgcn_sched_barrier(0);  // one slot's rows in flight at a time
         }
     }
     __syncthreads();
-    if (wave >= NCH) return;
+    if (wave >= NCH || wave >= nvalid) return;
 
     const int k = wave;
     const size_t c = (size_t)CS(k);
@@ -472,13 +577,21 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         if (lane == 0) {
             const int curp = cur > 0 ? cur - 1 : act - 1;  // :301-305
             int nf = (keep ^ FLAG_REV) | tag;
-            if (SCHED(k)) nf = (nf ^ FLAG_PWIN) | FLAG_LA | (la_dnew((int)c, a) << LA_D_SHIFT);
-            else if (!FULL(k)) nf |= FLAG_LA | ((la_jget(flags) + 1) << LA_J_SHIFT) | (la_dget(flags) << LA_D_SHIFT);
+            // far window: open (a far anchor this launch), advance, or drop
+            if (la_sched((int)c, a, LA_DF))
+                nf = (nf ^ FLAG_PWIN) | FLAG_LA | ((la_dnew((int)c, a, LA_DF) - 1) << LA_D_SHIFT);
+            else if (la_far_live(flags))
+                nf |= FLAG_LA | ((la_jf(flags) + 1) << LA_J_SHIFT) | ((la_df(flags) - 1) << LA_D_SHIFT);
+            // mid window
+            if (la_sched((int)c, a, LA_DM))
+                nf = (nf ^ FLAG_PWINM) | FLAG_LAM | ((la_dnew((int)c, a, LA_DM) - 1) << LA_DM_SHIFT);
+            else if (la_mid_live(flags))
+                nf |= FLAG_LAM | ((la_jm(flags) + 1) << LA_JM_SHIFT) | ((la_dm(flags) - 1) << LA_DM_SHIFT);
             J.state[c] = make_int4(curp, act, 0, nf);
         }
     } else {
         // output.fill(0); return (:278-281): the block stays in the input
-        // buffer, fill / current unchanged; the window is dropped
+        // buffer, fill / current unchanged; the windows are dropped
         const float *inc = J.in + c * J.in_stride;
         float *ibc = J.inbuf + c * B;
         for (int j = lane; j < B; j += 64) {
@@ -508,34 +621,39 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
         if (la_eligible<LOG2B>(st, J.n)) {
             const int c1[1] = {c};
             const int4 s1[1] = {st};
-            const bool f1[1] = {!((st.w & FLAG_LA) && la_jget(st.w) < la_dget(st.w))};
-            const bool h1[1] = {la_sched(c, a)};
-            la_step<LOG2B, NTL, 1>(a, J, c1, s1, f1, h1, 1, smem);
+            la_step<LOG2B, NTL, 1>(a, J, c1, s1, 1, smem);
         } else {
             process_job<LOG2B, LA_NT, false, NTL>(a, J, (size_t)c, st, smem);
         }
     }
 }
 
+// grid: [far anchors | mid anchors | step workgroups] (or the steps first)
 template <int LOG2B, bool NTL>
 __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
     using LS = LaStep<LOG2B>;
     constexpr int NCH = LS::NCH;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int nstep = (int)gridDim.x - a.la_nanchor;  // step workgroups
+    const int nanchor = a.la_nfar + a.la_nmid;
+    const int nstep = (int)gridDim.x - nanchor;  // step workgroups
     const int b = blockIdx.x;
     const int ba = a.la_steps_first ? b - nstep : b;  // anchor index, < 0 for a step
-    if (ba >= 0 && ba < a.la_nanchor) {
-        if (a.la_probe != 1) la_anchor<LOG2B, NTL>(a, ba, smem);
+    if (ba >= 0 && ba < nanchor) {
+        if (a.la_probe != 1) {
+            if (ba < a.la_nfar) {
+                if (a.la_probe != 4) la_anchor_far<LOG2B, NTL>(a, ba, smem);
+            } else if (a.la_probe != 3) {
+                la_anchor_mid<LOG2B, NTL>(a, ba - a.la_nfar);
+            }
+        }
         return;
     }
-    if (a.la_probe == 2) return;
-    const int c0 = (a.la_steps_first ? b : b - a.la_nanchor) * NCH;
+    if (a.la_probe >= 2) return;
+    const int c0 = (a.la_steps_first ? b : b - nanchor) * NCH;
     const ProcJob &J = a.job[0];
     const int nvalid = min(NCH, a.la_channels - c0);
     int cs[NCH];
     int4 st[NCH];
-    bool full[NCH], sched[NCH];
     bool all = true;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
@@ -545,10 +663,9 @@ __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
         st[k] = make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
                           __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
         all &= k >= nvalid || la_eligible<LOG2B>(st[k], J.n);
-        full[k] = !((st[k].w & FLAG_LA) && la_jget(st[k].w) < la_dget(st[k].w));
-        sched[k] = la_sched(cs[k], a);
     }
-    if (all) la_step<LOG2B, NTL, NCH>(a, J, cs, st, full, sched, nvalid, smem);
+    if (all)
+        la_step<LOG2B, NTL, NCH>(a, J, cs, st, nvalid, smem);
     else  // (the arguments by their kernarg address: no private copy of the block)
         la_fallback<LOG2B, NTL>((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), c0, nvalid, smem);
 }

@@ -1,8 +1,8 @@
 """The lookahead step (fft-convolution_amd/csrc/la.hpp) on the device.
 
 FFTConvolver::process (src/fft_convolver.rs:229-309) for a full block with
-the FDL sum re-associated in time: anchors sum the far rows' terms of the
-next 8 blocks ahead.  Checked against the oracle (tolerance REL_TOL, as every
+the FDL sum re-associated in time: mid anchors sum rows 5..16 four blocks
+ahead, far anchors rows >= 17 sixteen blocks ahead.  Checked against the oracle (tolerance REL_TOL, as every
 parity test), and for the property the design rests on -- the summation
 order is canonical, so the bits do not depend on a channel's stagger phase,
 its index, the shard it sits in, or whether a step was served from a window
@@ -60,7 +60,7 @@ def test_lookahead_vs_oracle(amd, oracle_mod, B):
 
 
 def test_lookahead_phase_independent(amd):
-    """13 identical channels sit at 8 different stagger phases (and anchor at
+    """13 identical channels sit at 13 different stagger phases (and anchor at
     different launches): every channel's output is bit-identical, through a
     partial call and a re-entry."""
     rng = np.random.default_rng(310)
@@ -100,7 +100,7 @@ def test_lookahead_shards_bitwise(amd):
     """A 24-channel batch split 7 + 17: every channel changes its stagger phase
     and its index, and the outputs stay bit-identical."""
     rng = np.random.default_rng(330)
-    C, B, L = 24, 256, 30 * 256
+    C, B, L = 24, 256, 40 * 256
     hs = np.stack([ir(rng, L) for _ in range(C)])
     one = amd.FFTConvolver.init(hs, B, L, channels=C)
     a = amd.FFTConvolver.init(hs[:7], B, L, channels=7)
