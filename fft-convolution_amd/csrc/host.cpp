@@ -307,7 +307,7 @@ struct UniformCore {
             a.la_seq = la_seq;
             // (far anchors: whole rounds of 8 channels, one XCD each -- see la_anchor_far)
             a.la_nfar = (int)((count((size_t)d.DF) + 7) / 8 * 8 * (size_t)d.wg_far);
-            a.la_nmid = (int)count((size_t)d.DM);
+            a.la_nmid = d.mid_in_step ? 0 : (int)count((size_t)d.DM);
             HIP_TRY(launch_process_la(log2b, a, (int)C, s));
             ++la_t;
             la_seq = 3 - la_seq;

@@ -149,8 +149,9 @@ size_t process_lds_bytes(int log2b);
 // lookahead: far parts (partial rows per step) for this geometry, 0 = not used
 int la_parts(int log2b, int S);
 struct LaDims {
-    int DF, DM;     // far / mid periods
-    int wg_far;     // workgroups per far anchor
+    int DF, DM;       // far / mid periods
+    int wg_far;       // workgroups per far anchor
+    int mid_in_step;  // the step workgroups run the mid anchors (no mid workgroups)
 };
 LaDims la_dims(int log2b);
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s);

@@ -144,12 +144,12 @@ __device__ __forceinline__ float4 *la_pm(const ProcArgs &a, size_t c, int win, i
 // rows in the chain's order.  X rows live in a register ring indexed by the
 // walk position e; each row of H and of the FDL is loaded once, LA_U ahead.
 // ---------------------------------------------------------------------------
-template <int LOG2B, bool ASC, bool NTL, int JW>
+template <int LOG2B, bool ASC, bool NTL, int JW, int U = LA_U>
 __device__ __forceinline__ void la_walk(LaAcc (&acc)[JW], const RowStream &hs, const RowStream &xs, int voff,
                                         bool z0, int lo, int hi, int j0, int cur, int act) {
     constexpr int ROWB = (1 << LOG2B) * (int)sizeof(float2);
-    constexpr int RS = JW + LA_U;                         // X ring: window + prefetch
-    constexpr int UNR = RS % LA_U == 0 ? RS : RS * LA_U;  // static ring slots
+    constexpr int RS = JW + U;                         // X ring: window + prefetch
+    constexpr int UNR = RS % U == 0 ? RS : RS * U;  // static ring slots
     const int n = hi - lo;
     const int ne = n + JW - 1;
     auto xoff = [&](int e) {
@@ -162,22 +162,22 @@ __device__ __forceinline__ void la_walk(LaAcc (&acc)[JW], const RowStream &hs, c
     // rows past the walk are loaded from an out-of-range buffer offset (zero,
     // no memory access): no branches around the loads, no register copies
     auto vo = [&](bool in) { return in ? voff : LA_OOB; };
-    float4 xr[RS], hr[LA_U];
+    float4 xr[RS], hr[U];
 #pragma unroll
     for (int e = 0; e < RS - 1; ++e) xr[e] = xs.ld4<NTL>(vo(e < ne), xoff(e < ne ? e : 0));
 #pragma unroll
-    for (int k = 0; k < LA_U; ++k) hr[k] = hs.ld4<NTL>(vo(k < n), hoff(k < n ? k : 0));
+    for (int k = 0; k < U; ++k) hr[k] = hs.ld4<NTL>(vo(k < n), hoff(k < n ? k : 0));
 #pragma nounroll
     for (int k0 = 0; k0 < n; k0 += UNR) {  // (not unrolled: a constant walk would hoist every load)
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             const int k = k0 + u;
             if (k >= n) break;
-            const LaH h = la_ops(hr[u % LA_U], z0);
+            const LaH h = la_ops(hr[u % U], z0);
 #pragma unroll
             for (int jj = 0; jj < JW; ++jj) acc[jj].mac(h, xr[(ASC ? u + JW - 1 - jj : u + jj) % RS]);
-            const bool hin = k + LA_U < n, xin = k + RS - 1 < ne;
-            hr[u % LA_U] = hs.ld4<NTL>(vo(hin), hoff(hin ? k + LA_U : 0));
+            const bool hin = k + U < n, xin = k + RS - 1 < ne;
+            hr[u % U] = hs.ld4<NTL>(vo(hin), hoff(hin ? k + U : 0));
             xr[(u + RS - 1) % RS] = xs.ld4<NTL>(vo(xin), xoff(xin ? k + RS - 1 : 0));
             // keep the issue order: the scheduler would otherwise hoist the
             // loads of later rows and run out of registers
@@ -334,7 +334,7 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
     LaAcc acc[JM];
 #pragma unroll
     for (int j = 0; j < JM; ++j) acc[j].zero();
-    la_walk<LOG2B, false, false, JM>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, l * JM, cur, act);
+    la_walk<LOG2B, false, false, JM, 2>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, l * JM, cur, act);
 #pragma unroll
     for (int j = 0; j < JM; ++j)
         if (l * JM + j < d) la_pm(a, c, win, l * JM + j, B)[f] = acc[j].get();
@@ -355,6 +355,10 @@ template <int LOG2B>
 struct LaStep {
     static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;
     static constexpr int NCH = LOG2B <= 8 ? 2 : 1;           // channels per step workgroup
+    // B <= 256: the step workgroup's helper waves (>= one laneset of F lanes
+    // after the pre) also run the mid anchors of its channels, after the
+    // pre, under the transform chains; B = 512 launches mid anchor workgroups
+    static constexpr bool MIDIN = LOG2B <= 8;
     // tw (2B float2) | per channel: bufA | bufB | H0 | pre (float2) | overlap | tail0 | tail1 (float)
     static constexpr size_t ch_bytes = 4 * 8 * (size_t)B + 3 * 4 * (size_t)B;
     static constexpr size_t chain_bytes = 16 * (size_t)B + NCH * ch_bytes;
@@ -538,7 +542,38 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         }
     }
     __syncthreads();
-    if (wave >= NCH || wave >= nvalid) return;
+    if (wave >= NCH) {
+        if constexpr (LS::MIDIN) {
+            // mid anchors of this workgroup's scheduled channels: rows DF..D1+1
+            // for the next DM steps (the pre-launch ring position is at hand)
+            constexpr int LH = HL / F;                    // helper lanesets
+            constexpr int JMS = LA_DM / (LH < LA_DM ? LH : LA_DM);
+            const int hl = tid - 64 * NCH;
+            const int l = __builtin_amdgcn_readfirstlane(hl / F), f = hl % F;
+            if (l * JMS < LA_DM) {
+#pragma unroll
+                for (int k = 0; k < NCH; ++k) {
+                    if (k >= nvalid || !la_sched(CS(k), a, LA_DM)) continue;
+                    const size_t c = (size_t)CS(k);
+                    const int cur = __builtin_amdgcn_readfirstlane(ST(k).x);
+                    const int act = __builtin_amdgcn_readfirstlane(ST(k).y);
+                    const int flags = __builtin_amdgcn_readfirstlane(ST(k).w);
+                    const int win = (flags & FLAG_PWINM) ? 0 : 1, d = la_dnew((int)c, a, LA_DM);
+                    const RowStream hs(J.H + c * rows, bytes), xs(J.X + c * rows, bytes);
+                    LaAcc acc[JMS];
+#pragma unroll
+                    for (int j = 0; j < JMS; ++j) acc[j].zero();
+                    la_walk<LOG2B, false, false, JMS, 2>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, l * JMS, cur,
+                                                         act);
+#pragma unroll
+                    for (int j = 0; j < JMS; ++j)
+                        if (l * JMS + j < d) la_pm(a, c, win, l * JMS + j, B)[f] = acc[j].get();
+                }
+            }
+        }
+        return;
+    }
+    if (wave >= nvalid) return;
 
     const int k = wave;
     const size_t c = (size_t)CS(k);
