@@ -13,7 +13,7 @@ enum : int {
     // lookahead (time-blocked FDL, see la.hpp): the far window of partial
     // sums is live (FLAG_LA) in P window FLAG_PWIN, bits 8-11 = steps of it
     // consumed, 12-15 = its length - 1; the mid window likewise (FLAG_LAM,
-    // FLAG_PWINM, bits 18-19, 20-21); bits 16-17 = the launch tag of the last
+    // FLAG_PWINM, bits 18-20, 21-23); bits 16-17 = the launch tag of the last
     // process launch that wrote this state word
     FLAG_LA = 16,
     FLAG_PWIN = 32,
@@ -23,8 +23,8 @@ enum : int {
     LA_D_SHIFT = 12,
     SEQ_SHIFT = 16,
     LA_JM_SHIFT = 18,
-    LA_DM_SHIFT = 20,
-    LA_MASK = FLAG_LA | FLAG_LAM | (15 << LA_J_SHIFT) | (15 << LA_D_SHIFT) | (3 << LA_JM_SHIFT) | (3 << LA_DM_SHIFT),
+    LA_DM_SHIFT = 21,
+    LA_MASK = FLAG_LA | FLAG_LAM | (15 << LA_J_SHIFT) | (15 << LA_D_SHIFT) | (7 << LA_JM_SHIFT) | (7 << LA_DM_SHIFT),
     SEQ_MASK = 3 << SEQ_SHIFT,
 };
 

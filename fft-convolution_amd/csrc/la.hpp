@@ -52,7 +52,7 @@ constexpr int LA_NT = 256;           // threads per workgroup (anchor and step r
 constexpr int LA_NG = 4;             // far-row groups
 constexpr int LA_CU = 8;             // full-pass chain: rows in flight per lane
 constexpr int LA_OOB = 0x7ffffff0;   // a buffer voffset past every stream's range
-static_assert(LA_DM <= LA_D1 && LA_DF % LA_JW == 0, "lookahead levels");
+static_assert(LA_DM <= LA_D1 && LA_DM <= 8 && LA_DF <= 16 && LA_DF % LA_JW == 0, "lookahead levels (state word fields)");
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -88,8 +88,8 @@ struct LaAcc {
 // mid window {FLAG_LAM, FLAG_PWINM, jm, dm-1}
 __device__ __forceinline__ int la_jf(int w) { return (w >> LA_J_SHIFT) & 15; }
 __device__ __forceinline__ int la_df(int w) { return ((w >> LA_D_SHIFT) & 15) + 1; }
-__device__ __forceinline__ int la_jm(int w) { return (w >> LA_JM_SHIFT) & 3; }
-__device__ __forceinline__ int la_dm(int w) { return ((w >> LA_DM_SHIFT) & 3) + 1; }
+__device__ __forceinline__ int la_jm(int w) { return (w >> LA_JM_SHIFT) & 7; }
+__device__ __forceinline__ int la_dm(int w) { return ((w >> LA_DM_SHIFT) & 7) + 1; }
 __device__ __forceinline__ bool la_far_live(int w) { return (w & FLAG_LA) && la_jf(w) < la_df(w); }
 __device__ __forceinline__ bool la_mid_live(int w) { return (w & FLAG_LAM) && la_jm(w) < la_dm(w); }
 
@@ -285,9 +285,11 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
     LaAcc acc[LA_JW];
 #pragma unroll
     for (int j = 0; j < LA_JW; ++j) acc[j].zero();
+    // (plain loads: the nontemporal policy streamed no faster here and cost the
+    // step workgroups' cache-resident near rows ~8 % of the launch, r1i_la15_ab)
     if (hi > lo) {
-        if (g & 1) la_walk<LOG2B, true, NTL, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
-        else la_walk<LOG2B, false, NTL, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        if (g & 1) la_walk<LOG2B, true, false, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        else la_walk<LOG2B, false, false, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
     }
     if constexpr (GPW > 1) {
         float4 *red = reinterpret_cast<float4 *>(smem);  // [GPW-1][JW][F]
