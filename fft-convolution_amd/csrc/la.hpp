@@ -540,7 +540,6 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             for (int i = LA_D1; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
             float2 *prel = reinterpret_cast<float2 *>(chan_lds(k)) + 3 * B;
             reinterpret_cast<float4 *>(prel)[f] = vadd(acc.get(), vadd(M, A));
-            __builtin_amdgcn_sched_barrier(0);  // one slot's rows in flight at a time
         }
     }
     __syncthreads();
