@@ -218,6 +218,7 @@ struct LaGeo {
     // one anchor = WF parts x (DF / JW) halves, XCD-aligned (see la_anchor_far)
     static constexpr int GPW = LPW < LA_NG ? LPW : LA_NG;
     static constexpr int WF = LA_NG / GPW;                          // far parts (P rows per step)
+    static_assert(LA_NG % GPW == 0, "far groups must fill whole parts");
     static constexpr int WG_FAR = WF * (LA_DF / LA_JW);             // workgroups per far anchor
     static constexpr int JM = LA_DM / (LPW > LA_DM ? LA_DM : LPW);  // mid window steps per laneset
     static constexpr size_t anchor_bytes = (size_t)(GPW - 1) * LA_JW * F * 16;
