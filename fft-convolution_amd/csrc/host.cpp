@@ -852,6 +852,17 @@ struct CrossfadeCore {
         }
         const size_t m = max_buffer_size;
         if (m > (size_t)INT32_MAX) return fail(FFTCONV_E_UNSUPPORTED, "process length exceeds 2^31-1");
+        if (m > 0 && C > 0 && m == a->B && a->la_W && b->la_W && la_parts(a->log2b, (int)a->S) == a->la_W &&
+            la_parts(b->log2b, (int)b->S) == b->la_W) {
+            // :72-73 on the lookahead step: each convolver's full
+            // block runs its own launch of far / mid anchors and steps; then
+            // the mix (:75-77)
+            if (int r = a->process_device(din, is, buf_a.p, m, m, s)) return r;
+            if (int r = b->process_device(din, is, buf_b.p, m, m, s)) return r;
+            HIP_TRY(launch_crossfade_mix(mix_args(dout, os, out_len), (int)C, s));
+            xf.advance(out_len);
+            return FFTCONV_OK;
+        }
         if (m > 0 && C > 0) {
             // :72-73 -- A and B are two jobs of ONE launch (same block size):
             // 2C workgroups fill the chip where C alone leaves it half occupied

@@ -23,6 +23,9 @@ import torch
 import fftconv_amd as F
 from fftconv_amd import shard
 
+sys.path.insert(0, ROOT)
+from bench import lookahead_bytes_per_channel_block  # noqa: E402
+
 
 def uniform_bytes(B, L):
     S = -(-L // B)
@@ -76,7 +79,9 @@ def main():
                    help="cfg3 only: ';'-separated knob sets (e.g. 'lag=0;lag=32;variant=4') timed "
                         "interleaved in this process, --rounds times")
     p.add_argument("--rounds", type=int, default=4)
+    p.add_argument("--variant", type=int, default=-1, help="fftconv_set_kernel_variant for every config")
     a = p.parse_args()
+    F.set_kernel_variant(a.variant)
     torch.cuda.set_device(0)
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
@@ -127,12 +132,18 @@ def main():
 
         t, ev = run(conv, C, B, B, a.steps5, 64, 16, s, update=upd)
         samples = C * B * a.steps5
-        per_sample = 2 * uniform_bytes(B, L) / B
+        # both inner convolvers on the lookahead step unless variant bit 4 is set
+        la = a.variant < 0 or not (a.variant & 16)
+        parts = 4 // min(512 // B, 4)
+        per_sample = 2 * (lookahead_bytes_per_channel_block(B, L, parts) if la else uniform_bytes(B, L)) / B
         out.append({"config": "cfg5 CrossfadeConvolver, update every 128 blocks", "channels": C, "block": B,
                     "ir": L, "steps": a.steps5, "MSamples_s": round(samples / t / 1e6, 2),
                     "us_per_step": round(t / a.steps5 * 1e6, 3),
+                    "path": "lookahead step (two launches) + mix" if la else "full-sum pair launch",
                     "algorithmic_GBs_incl_updates": round(samples * per_sample / t / 1e9, 1),
+                    "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
                     "bytes_per_sample": round(per_sample, 1),
+                    "canonical_bytes_per_sample": round(2 * uniform_bytes(B, L) / B, 1),
                     "note": "update_device() (HBM-resident IRs: S-segment FFTs per channel) is inside the timed region"})
     for o in out:
         print(json.dumps(o), flush=True)

@@ -172,3 +172,42 @@ def test_lookahead_device_steps(amd, oracle_mod):
         ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
         assert_close(y[c], np.concatenate([ref.process(x[c, k * B:(k + 1) * B]) for k in range(K)]),
                      what=f"channel {c}")
+
+
+@pytest.mark.parametrize("B,L", [(256, 40 * 256 + 5), (512, 36 * 512)])
+def test_lookahead_crossfade_vs_oracle(amd, oracle_mod, B, L):
+    """CrossfadeConvolver<FFTConvolver> (src/crossfade_convolver.rs:45-105)
+    with both inner convolvers on the lookahead step: immediate and pending
+    IR swaps (the trait init fades over the response length), against the
+    oracle every block, and against the full-sum kernels within f32 rounding."""
+    rng = np.random.default_rng(370 + B)
+    C = 3
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    blocks = 70
+    ups = {5: L, 17: L - 3 * B, 30: L, 52: L - B // 2}
+    xs = [np.stack([white(rng, B) for _ in range(C)]) for _ in range(blocks)]
+    news = {i: np.stack([ir(rng, n) for _ in range(C)]) for i, n in ups.items()}
+    refs = [oracle_mod.CrossfadeConvolver.init(hs[c], B, L) for c in range(C)]
+    outs = {}
+    for v in (-1, NOLA):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.CrossfadeConvolver.init(hs, B, L, channels=C)
+            ys = []
+            for i in range(blocks):
+                if i in news:
+                    conv.update(news[i])
+                ys.append(conv.process(xs[i]))
+            outs[v] = np.concatenate(ys, axis=1)
+        finally:
+            amd.set_kernel_variant(-1)
+    exp = []
+    for i in range(blocks):
+        if i in news:
+            for c in range(C):
+                refs[c].update(news[i][c])
+        exp.append(np.stack([refs[c].process(xs[i][c]) for c in range(C)]))
+    exp = np.concatenate(exp, axis=1)
+    for c in range(C):
+        assert_close(outs[-1][c], exp[c], what=f"lookahead ch {c}")
+        assert_close(outs[NOLA][c], exp[c], what=f"full-sum ch {c}")
