@@ -7,8 +7,8 @@ f32.  One *step* = one FFTConvolver::process call of 256 samples on every
 channel (src/fft_convolver.rs:229-309) = one fused kernel launch: forward R2C
 of the new block into the FDL, the S-segment spectral MAC, C2R and overlap-add
 -- with the lookahead step (csrc/la.hpp) the FDL rows beyond the 4 nearest are
-summed ahead by the launch's anchor workgroups (rows 5..16 four blocks ahead
-for C/4 channels, rows >= 17 sixteen blocks ahead for C/16 channels).
+summed ahead by the launch's anchor workgroups (rows 5..32 four blocks ahead
+for C/4 channels, rows >= 33 thirty-two blocks ahead for C/32 channels).
 Inputs are resident in HBM when the timed region starts.
 
 Multi-GPU (BASELINE configs[3], 8192 channels on 8 GPUs): one process per GPU,
@@ -47,7 +47,7 @@ def algorithmic_bytes_per_channel_block(B: int, L: int) -> int:
     return 16 * S * K + 8 * K + 4 * B + 4 * B + 8 * B
 
 
-LA_D1, LA_DM, LA_DF = 4, 4, 16  # lookahead levels (fft-convolution_amd/csrc/la.hpp)
+LA_D1, LA_DM, LA_DF = 4, 4, 32  # lookahead levels (fft-convolution_amd/csrc/la.hpp)
 
 
 def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
@@ -60,7 +60,7 @@ def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
       near rows (step): H[1..D1] and the last D1 blocks: 8K * 2 D1;
       window rows written by the anchors and read by the steps: 16K (parts + 1);
       the new X row, H[0], in, out, overlap r/w: 16K + 16B.
-    cfg2 (parts 2): 96,744 B, against 779,208 B for the reference's
+    cfg2 (parts 2): 89,228 B, against 779,208 B for the reference's
     algorithm (every block streams all S rows of H and of the FDL)."""
     S = -(-L // B)
     K = B + 1
@@ -106,6 +106,8 @@ def pmc_traffic(args):
     prof = shutil.which("rocprofv3")
     if not prof:
         return None, "rocprofv3 not found"
+    if any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None, "already under rocprofv3: no nested --pmc pass"
     env = dict(os.environ, TMPDIR="/tmp")
     vals = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):

@@ -1251,7 +1251,7 @@ hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_
 int la_parts(int log2b, int S) {
     if (log2b < 7 || log2b > 9) return 0;
     if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NOLA)) return 0;
-    if (S < 2 * LA_DF) return 0;
+    if (S < LA_DF + 8) return 0;  // (channels whose active segments drop below DF + 2 step generically)
     switch (log2b) {
         case 7: return LaGeo<7>::WF;
         case 8: return LaGeo<8>::WF;

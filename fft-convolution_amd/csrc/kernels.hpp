@@ -11,20 +11,20 @@ enum : int {
     FLAG_PRE = 4,    // pre[] holds pre_multiplied of the block that starts at `current`
     FLAG_XSYNC = 8,  // crossfade pair: this FDL has always equalled its partner's
     // lookahead (time-blocked FDL, see la.hpp): the far window of partial
-    // sums is live (FLAG_LA) in P window FLAG_PWIN, bits 8-11 = steps of it
-    // consumed, 12-15 = its length - 1; the mid window likewise (FLAG_LAM,
-    // FLAG_PWINM, bits 18-20, 21-23); bits 16-17 = the launch tag of the last
+    // sums is live (FLAG_LA) in P window FLAG_PWIN, bits 8-12 = steps of it
+    // consumed, 13-17 = its length - 1; the mid window likewise (FLAG_LAM,
+    // FLAG_PWINM, bits 18-20, 21-23); bits 24-25 = the launch tag of the last
     // process launch that wrote this state word
     FLAG_LA = 16,
     FLAG_PWIN = 32,
     FLAG_LAM = 64,
     FLAG_PWINM = 128,
     LA_J_SHIFT = 8,
-    LA_D_SHIFT = 12,
-    SEQ_SHIFT = 16,
+    LA_D_SHIFT = 13,
     LA_JM_SHIFT = 18,
     LA_DM_SHIFT = 21,
-    LA_MASK = FLAG_LA | FLAG_LAM | (15 << LA_J_SHIFT) | (15 << LA_D_SHIFT) | (7 << LA_JM_SHIFT) | (7 << LA_DM_SHIFT),
+    SEQ_SHIFT = 24,
+    LA_MASK = FLAG_LA | FLAG_LAM | (31 << LA_J_SHIFT) | (31 << LA_D_SHIFT) | (7 << LA_JM_SHIFT) | (7 << LA_DM_SHIFT),
     SEQ_MASK = 3 << SEQ_SHIFT,
 };
 

@@ -15,6 +15,7 @@
 //                          the DM steps after it (X ages >= 1 at the anchor);
 //   far rows   DF+1..act-1 summed by a *far anchor* every DF steps, for the
 //                          DF steps after it.
+// (D1 = DM = 4, DF = 32: r1j A/B, DF = 16 was 9.5 % slower at cfg2.)
 // An anchor walks its rows once, keeping a window of X rows in registers, and
 // leaves one partial-sum row per future step (P windows in HBM).  Per channel-
 // block the far rows then cost 16 B (S - DF) / DF per bin instead of 16 B S,
@@ -45,14 +46,14 @@
 
 constexpr int LA_D1 = 4;             // near rows, summed by the step
 constexpr int LA_DM = 4;             // mid period / window (<= LA_D1)
-constexpr int LA_DF = 16;            // far period / window; mid rows are D1+1..DF
+constexpr int LA_DF = 32;            // far period / window; mid rows are D1+1..DF
 constexpr int LA_JW = 8;             // far window steps per laneset (register window)
 constexpr int LA_U = 2;              // anchor: H / X rows in flight per lane
 constexpr int LA_NT = 256;           // threads per workgroup (anchor and step roles)
 constexpr int LA_NG = 4;             // far-row groups
 constexpr int LA_CU = 8;             // full-pass chain: rows in flight per lane
 constexpr int LA_OOB = 0x7ffffff0;   // a buffer voffset past every stream's range
-static_assert(LA_DM <= LA_D1 && LA_DM <= 8 && LA_DF <= 16 && LA_DF % LA_JW == 0, "lookahead levels (state word fields)");
+static_assert(LA_DM <= LA_D1 && LA_DM <= 8 && LA_DF <= 32 && LA_DF % LA_JW == 0, "lookahead levels (state word fields)");
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -86,8 +87,8 @@ struct LaAcc {
 
 // state word fields (kernels.hpp): far window {FLAG_LA, FLAG_PWIN, j, d-1},
 // mid window {FLAG_LAM, FLAG_PWINM, jm, dm-1}
-__device__ __forceinline__ int la_jf(int w) { return (w >> LA_J_SHIFT) & 15; }
-__device__ __forceinline__ int la_df(int w) { return ((w >> LA_D_SHIFT) & 15) + 1; }
+__device__ __forceinline__ int la_jf(int w) { return (w >> LA_J_SHIFT) & 31; }
+__device__ __forceinline__ int la_df(int w) { return ((w >> LA_D_SHIFT) & 31) + 1; }
 __device__ __forceinline__ int la_jm(int w) { return (w >> LA_JM_SHIFT) & 7; }
 __device__ __forceinline__ int la_dm(int w) { return ((w >> LA_DM_SHIFT) & 7) + 1; }
 __device__ __forceinline__ bool la_far_live(int w) { return (w & FLAG_LA) && la_jf(w) < la_df(w); }
