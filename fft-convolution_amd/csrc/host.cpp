@@ -303,7 +303,7 @@ struct UniformCore {
             a.laPm = laPm.p;
             a.la_W = la_W;
             a.la_all = la_all ? 1 : 0;
-            a.la_t = (int)(la_t % (unsigned long long)d.DF);
+            a.la_t = (int)(la_t % (unsigned long long)(d.DF * d.DM));  // (both periods divide it)
             a.la_seq = la_seq;
             // (far anchors: whole rounds of 8 channels, one XCD each -- see la_anchor_far)
             a.la_nfar = (int)((count((size_t)d.DF) + 7) / 8 * 8 * (size_t)d.wg_far);

@@ -97,7 +97,7 @@ struct ProcArgs {
     int la_nfar;           // far anchor workgroups at the front of the grid
     int la_nmid;           // mid anchor workgroups after them
     int la_all;            // 1: every channel is scheduled for anchors (entry launch); -1: none is
-    int la_t;              // launch counter mod LA_DF: channel c anchors at period P when (c - t) % P == 0
+    int la_t;              // launch counter mod LA_DF*LA_DM: channel c anchors at period P when (c - t) % P == 0
     int la_seq;            // 1 or 2, alternating per lookahead launch; 0 in every other launch
     int la_steps_first;    // grid order: step workgroups before the anchors (tuning)
     int la_probe;          // timing probe only (wrong results): 1 = anchors idle, 2 = steps idle,

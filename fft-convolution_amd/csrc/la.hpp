@@ -44,11 +44,13 @@
 #pragma once
 // (no namespace of its own: included inside namespace fftconv)
 
-constexpr int LA_D1 = 4;             // near rows, summed by the step
-constexpr int LA_DM = 4;             // mid period / window (<= LA_D1)
+constexpr int LA_D1 = 5;             // near rows, summed by the step
+constexpr int LA_DM = 5;             // mid period / window (<= LA_D1)
 constexpr int LA_DF = 32;            // far period / window; mid rows are D1+1..DF
 constexpr int LA_JW = 8;             // far window steps per laneset (register window)
 constexpr int LA_U = 2;              // anchor: H / X rows in flight per lane
+constexpr int LA_UF = 2;             // far anchor: H / X rows in flight per lane
+constexpr int LA_UM = 2;             // mid anchor: H / X rows in flight per lane
 constexpr int LA_NT = 256;           // threads per workgroup (anchor and step roles)
 constexpr int LA_NG = 4;             // far-row groups
 constexpr int LA_CU = 8;             // full-pass chain: rows in flight per lane
@@ -100,7 +102,7 @@ template <int LOG2B>
 __device__ __forceinline__ bool la_eligible(int4 st, int n) {
     return n == (1 << LOG2B) && st.z == 0 && !(st.w & FLAG_INBUF) && st.y >= LA_DF + 2 && st.x < st.y;
 }
-// stagger phase of channel c at level period P (la_t = launch counter mod DF)
+// stagger phase of channel c at level period P (la_t = launch counter mod DF*DM)
 __device__ __forceinline__ int la_phase(int c, const ProcArgs &a, int P) {
     const int r = (c - a.la_t) % P;
     return r < 0 ? r + P : r;
@@ -113,6 +115,11 @@ __device__ __forceinline__ int la_dnew(int c, const ProcArgs &a, int P) {
     const int r = la_phase(c, a, P);
     return r == 0 ? P : r;
 }
+// mid window split over L lanesets: ceil(DM / L) steps each; the last laneset's
+// run is shifted back to end at step DM (no step past the window: its rows
+// would meet blocks not yet written) and stores only the steps it owns
+__host__ __device__ constexpr int la_mid_per(int L) { return (LA_DM + (L < LA_DM ? L : LA_DM) - 1) / (L < LA_DM ? L : LA_DM); }
+__device__ __forceinline__ int la_mid_j0(int l, int JM) { return min(l * JM, LA_DM - JM); }
 // far-row group g of NG: rows [lo, hi) of [DF+1, act)
 __device__ __forceinline__ void la_group(int g, int act, int &lo, int &hi) {
     const int nf = act - LA_DF - 1;
@@ -221,7 +228,7 @@ struct LaGeo {
     static constexpr int WF = LA_NG / GPW;                          // far parts (P rows per step)
     static_assert(LA_NG % GPW == 0, "far groups must fill whole parts");
     static constexpr int WG_FAR = WF * (LA_DF / LA_JW);             // workgroups per far anchor
-    static constexpr int JM = LA_DM / (LPW > LA_DM ? LA_DM : LPW);  // mid window steps per laneset
+    static constexpr int JM = la_mid_per(LPW);                      // mid window steps per laneset
     static constexpr size_t anchor_bytes = (size_t)(GPW - 1) * LA_JW * F * 16;
 };
 
@@ -268,7 +275,7 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
     // then serves the rows the window halves and neighbouring groups share
     const int x = b & 7, y = b >> 3;
     const int ci = (y / LG::WG_FAR) * 8 + x, r = y % LG::WG_FAR;
-    const int c = a.la_all > 0 ? ci : a.la_t + LA_DF * ci;
+    const int c = a.la_all > 0 ? ci : (a.la_t % LA_DF) + LA_DF * ci;
     if (c >= a.la_channels) return;  // (padding of the last XCD round)
     int cur, act, win, d;
     if (!la_anchor_state<LOG2B>(a, c, LA_DF, cur, act, win, d)) return;
@@ -290,8 +297,8 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
     // (plain loads: the nontemporal policy streamed no faster here and cost the
     // step workgroups' cache-resident near rows ~8 % of the launch, r1i_la15_ab)
     if (hi > lo) {
-        if (g & 1) la_walk<LOG2B, true, false, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
-        else la_walk<LOG2B, false, false, LA_JW>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        if (g & 1) la_walk<LOG2B, true, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        else la_walk<LOG2B, false, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
     }
     if constexpr (GPW > 1) {
         float4 *red = reinterpret_cast<float4 *>(smem);  // [GPW-1][JW][F]
@@ -332,16 +339,17 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
     const int tid = threadIdx.x;
     const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
     if (l * JM >= LA_DM) return;  // (more lanesets than window steps)
+    const int j0 = la_mid_j0(l, JM);
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
     const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
     LaAcc acc[JM];
 #pragma unroll
     for (int j = 0; j < JM; ++j) acc[j].zero();
-    la_walk<LOG2B, false, false, JM, 2>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, l * JM, cur, act);
+    la_walk<LOG2B, false, false, JM, LA_UM>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, j0, cur, act);
 #pragma unroll
     for (int j = 0; j < JM; ++j)
-        if (l * JM + j < d) la_pm(a, c, win, l * JM + j, B)[f] = acc[j].get();
+        if (j0 + j >= l * JM && j0 + j < d) la_pm(a, c, win, j0 + j, B)[f] = acc[j].get();
 }
 
 // ---------------------------------------------------------------------------
@@ -546,11 +554,12 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     }
     __syncthreads();
     if (wave >= NCH) {
+        if (a.la_probe >= 5) return;  // (timing probes 5/6: steps without their mid anchors)
         if constexpr (LS::MIDIN) {
             // mid anchors of this workgroup's scheduled channels: rows DF..D1+1
             // for the next DM steps (the pre-launch ring position is at hand)
             constexpr int LH = HL / F;                    // helper lanesets
-            constexpr int JMS = LA_DM / (LH < LA_DM ? LH : LA_DM);
+            constexpr int JMS = la_mid_per(LH);
             const int hl = tid - 64 * NCH;
             const int l = __builtin_amdgcn_readfirstlane(hl / F), f = hl % F;
             if (l * JMS < LA_DM) {
@@ -566,11 +575,12 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                     LaAcc acc[JMS];
 #pragma unroll
                     for (int j = 0; j < JMS; ++j) acc[j].zero();
-                    la_walk<LOG2B, false, false, JMS, 2>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, l * JMS, cur,
+                    const int j0 = la_mid_j0(l, JMS);
+                    la_walk<LOG2B, false, false, JMS, LA_UM>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, j0, cur,
                                                          act);
 #pragma unroll
                     for (int j = 0; j < JMS; ++j)
-                        if (l * JMS + j < d) la_pm(a, c, win, l * JMS + j, B)[f] = acc[j].get();
+                        if (j0 + j >= l * JMS && j0 + j < d) la_pm(a, c, win, j0 + j, B)[f] = acc[j].get();
                 }
             }
         }
@@ -677,7 +687,7 @@ __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
     const int b = blockIdx.x;
     const int ba = a.la_steps_first ? b - nstep : b;  // anchor index, < 0 for a step
     if (ba >= 0 && ba < nanchor) {
-        if (a.la_probe != 1) {
+        if (a.la_probe != 1 && a.la_probe != 6) {
             if (ba < a.la_nfar) {
                 if (a.la_probe != 4) la_anchor_far<LOG2B, NTL>(a, ba, smem);
             } else if (a.la_probe != 3) {
@@ -686,7 +696,7 @@ __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
         }
         return;
     }
-    if (a.la_probe >= 2) return;
+    if (a.la_probe >= 2 && a.la_probe <= 4) return;
     const int c0 = (a.la_steps_first ? b : b - nanchor) * NCH;
     const ProcJob &J = a.job[0];
     const int nvalid = min(NCH, a.la_channels - c0);
