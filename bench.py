@@ -60,7 +60,7 @@ def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
       near rows (step): H[1..D1] and the last D1 blocks: 8K * 2 D1;
       window rows written by the anchors and read by the steps: 16K (parts + 1);
       the new X row, H[0], in, out, overlap r/w: 16K + 16B.
-    cfg2 (parts 2): 86,862 B, against 779,208 B for the reference's
+    cfg2 (parts 1): 82,750 B, against 779,208 B for the reference's
     algorithm (every block streams all S rows of H and of the FDL)."""
     S = -(-L // B)
     K = B + 1

@@ -222,14 +222,17 @@ __device__ __forceinline__ void la_chain(LaAcc &acc, const RowStream &hs, const 
 template <int LOG2B>
 struct LaGeo {
     static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;  // lanesets of F lanes per workgroup
-    // far anchor workgroup: GPW groups (one per laneset) of one window half;
-    // one anchor = WF parts x (DF / JW) halves, XCD-aligned (see la_anchor_far)
-    static constexpr int GPW = LPW < LA_NG ? LPW : LA_NG;
+    // far anchor workgroup: one bin slice of FS lanes (bins are independent),
+    // GPW far groups (one wave-sized laneset each) of one window slice of JW
+    // steps, combined in LDS; one anchor = NSL slices x WF parts x (DF / JW)
+    // window slices, XCD-aligned (see la_anchor_far)
+    static constexpr int FS = F < 64 ? F : 64, NSL = F / FS, LPF = LA_NT / FS;
+    static constexpr int GPW = LPF < LA_NG ? LPF : LA_NG;
     static constexpr int WF = LA_NG / GPW;                          // far parts (P rows per step)
     static_assert(LA_NG % GPW == 0, "far groups must fill whole parts");
-    static constexpr int WG_FAR = WF * (LA_DF / LA_JW);             // workgroups per far anchor
+    static constexpr int WG_FAR = NSL * WF * (LA_DF / LA_JW);       // workgroups per far anchor
     static constexpr int JM = la_mid_per(LPW);                      // mid window steps per laneset
-    static constexpr size_t anchor_bytes = (size_t)(GPW - 1) * LA_JW * F * 16;
+    static constexpr size_t anchor_bytes = (size_t)(GPW - 1) * LA_JW * FS * 16;
 };
 
 // the anchor's view of channel c: its ring position, window and length, or
@@ -268,7 +271,7 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int c, int P,
 template <int LOG2B, bool NTL>
 __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned char *smem) {
     using LG = LaGeo<LOG2B>;
-    constexpr int B = LG::B, F = LG::F, GPW = LG::GPW;
+    constexpr int B = LG::B, GPW = LG::GPW;
     const ProcJob &J = a.job[0];
     // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so the
     // WG_FAR workgroups of one anchor sit 8 apart -- on one XCD, whose L2
@@ -280,11 +283,13 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
     int cur, act, win, d;
     if (!la_anchor_state<LOG2B>(a, c, LA_DF, cur, act, win, d)) return;
 
+    constexpr int FS = LG::FS, NSL = LG::NSL;
     const int tid = threadIdx.x;
-    const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
+    const int l = __builtin_amdgcn_readfirstlane(tid / FS), fl = tid % FS;
     if (l >= GPW) return;                              // (more lanesets than groups)
-    const int w = r % LG::WF;                          // part
-    const int h = r / LG::WF;                          // window half: steps h*JW+1 .. h*JW+JW
+    const int f = (r % NSL) * FS + fl;                 // bin slice
+    const int w = (r / NSL) % LG::WF;                  // part
+    const int h = r / (NSL * LG::WF);                  // window slice: steps h*JW+1 .. h*JW+JW
     const int g = w * GPW + l;
     int lo, hi;
     la_group(g, act, lo, hi);
@@ -301,10 +306,10 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
         else la_walk<LOG2B, false, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
     }
     if constexpr (GPW > 1) {
-        float4 *red = reinterpret_cast<float4 *>(smem);  // [GPW-1][JW][F]
+        float4 *red = reinterpret_cast<float4 *>(smem);  // [GPW-1][JW][FS]
         if (l > 0) {
 #pragma unroll
-            for (int j = 0; j < LA_JW; ++j) red[((l - 1) * LA_JW + j) * F + f] = acc[j].get();
+            for (int j = 0; j < LA_JW; ++j) red[((l - 1) * LA_JW + j) * FS + fl] = acc[j].get();
         }
         __syncthreads();
         if (l == 0) {
@@ -313,7 +318,7 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
                 if (h * LA_JW + j < d) {
                     float4 p = acc[j].get();
 #pragma unroll
-                    for (int q = 1; q < GPW; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * F + f]);
+                    for (int q = 1; q < GPW; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * FS + fl]);
                     la_pf(a, c, win, h * LA_JW + j, w, B)[f] = p;
                 }
             }

@@ -134,7 +134,7 @@ def main():
         samples = C * B * a.steps5
         # both inner convolvers on the lookahead step unless variant bit 4 is set
         la = a.variant < 0 or not (a.variant & 16)
-        parts = 4 // min(512 // B, 4)
+        parts = 1  # far window parts (LaGeo::WF: 4 far groups, one bin slice per 4-wave workgroup)
         per_sample = 2 * (lookahead_bytes_per_channel_block(B, L, parts) if la else uniform_bytes(B, L)) / B
         out.append({"config": "cfg5 CrossfadeConvolver, update every 128 blocks", "channels": C, "block": B,
                     "ir": L, "steps": a.steps5, "MSamples_s": round(samples / t / 1e6, 2),
