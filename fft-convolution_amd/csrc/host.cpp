@@ -283,7 +283,10 @@ struct UniformCore {
         return j;
     }
 
-    int process_device(const float *din, size_t is, float *dout, size_t os, size_t n, hipStream_t s) {
+    // la_mix / mix / mix_tab: crossfade fusion on the lookahead step (ProcArgs::la_mix);
+    // the caller only passes them when this call takes the lookahead launch
+    int process_device(const float *din, size_t is, float *dout, size_t os, size_t n, hipStream_t s,
+                       int la_mix = 0, const CrossfadeMixArgs *mix = nullptr, float *mix_tab = nullptr) {
         if (n > (size_t)INT32_MAX) return fail(FFTCONV_E_UNSUPPORTED, "process length exceeds 2^31-1");
         if (n == 0 || C == 0) return FFTCONV_OK;
         ProcArgs a{};
@@ -308,6 +311,11 @@ struct UniformCore {
             // (far anchors: whole rounds of 8 channels, one XCD each -- see la_anchor_far)
             a.la_nfar = (int)((count((size_t)d.DF) + 7) / 8 * 8 * (size_t)d.wg_far);
             a.la_nmid = d.mid_in_step ? 0 : (int)count((size_t)d.DM);
+            if (la_mix && mix) {
+                a.la_mix = la_mix;
+                a.mix = *mix;
+                a.mix_tab = mix_tab;
+            }
             HIP_TRY(launch_process_la(log2b, a, (int)C, s));
             ++la_t;
             la_seq = 3 - la_seq;
@@ -700,6 +708,7 @@ struct CrossfadeCore {
     std::unique_ptr<UniformCore> a, b;
     Crossfader xf;
     DevPtr<float> buf_a, buf_b, stored;
+    DevPtr<float> mix_tab;  // [max_buffer_size + 1] mix_value walk (lookahead-fused mix)
     bool response_pending = false;
     hipStream_t stream = nullptr;
     Scratch scratch;
@@ -748,6 +757,7 @@ struct CrossfadeCore {
         max_buffer_size = mbs;
         if (int r = buf_a.alloc(C * mbs)) return r;
         if (int r = buf_b.alloc(C * mbs)) return r;
+        if (int r = mix_tab.alloc(mbs + 1)) return r;
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -857,6 +867,16 @@ struct CrossfadeCore {
             // :72-73 on the lookahead step: each convolver's full
             // block runs its own launch of far / mid anchors and steps; then
             // the mix (:75-77)
+            if (out_len == m && la_fuse_mix_allowed()) {
+                // the mix fused into B's launch: A's launch walks mix_value
+                // once into mix_tab, B's epilogue mixes A's block (buf_a) with
+                // its own straight into the output -- no mix launch, no buf_b
+                const CrossfadeMixArgs mx = mix_args(dout, os, out_len);
+                if (int r = a->process_device(din, is, buf_a.p, m, m, s, 1, &mx, mix_tab.p)) return r;
+                if (int r = b->process_device(din, is, dout, os, m, s, 2, &mx, mix_tab.p)) return r;
+                xf.advance(out_len);
+                return FFTCONV_OK;
+            }
             if (int r = a->process_device(din, is, buf_a.p, m, m, s)) return r;
             if (int r = b->process_device(din, is, buf_b.p, m, m, s)) return r;
             HIP_TRY(launch_crossfade_mix(mix_args(dout, os, out_len), (int)C, s));
@@ -922,6 +942,7 @@ struct CrossfadeCore {
         if (int r = b->clone_from(*o.b)) return r;
         if (int r = buf_a.alloc(o.buf_a.n)) return r;
         if (int r = buf_b.alloc(o.buf_b.n)) return r;
+        if (int r = mix_tab.alloc(o.mix_tab.n)) return r;
         if (int r = stored.alloc(o.stored.n)) return r;
         if (stored.n) HIP_TRY(hipMemcpyAsync(stored.p, o.stored.p, stored.bytes(), hipMemcpyDeviceToDevice, stream));
         HIP_TRY(hipStreamSynchronize(stream));
@@ -980,7 +1001,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 63) return fail(FFTCONV_E_INVALID, "variant must be 0..63 (or -1 = auto)");
+    if (variant > 127) return fail(FFTCONV_E_INVALID, "variant must be 0..127 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }

@@ -791,8 +791,6 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
     if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
 }
 
-#include "la.hpp"
-
 template <int LOG2B, int NT, bool ZZ, bool NTL>
 __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -810,6 +808,18 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
 // ---------------------------------------------------------------------------
 // Crossfader::mix for sample j of the call.  vtab (if given) holds the
 // sequential mix_value walk: vtab[k] = mix_value0 + step + ... (k adds).
+// RaisedCosineMixer (:160-169): gain g1 = cos^2(pi/2 * v) of A, 1 - g1 of B
+__device__ __forceinline__ float mix_gain(float v) {
+    const float PI_HALF = 3.14159265358979323846f * 0.5f;
+    const float rad = __fmul_rn(PI_HALF, v);
+    const float cs = cosf(rad);
+    return __fmul_rn(cs, cs);
+}
+__device__ __forceinline__ float mix_apply(float va, float vb, float g1) {
+    const float g2 = __fsub_rn(1.0f, g1);
+    return __fadd_rn(__fmul_rn(va, g1), __fmul_rn(vb, g2));
+}
+
 __device__ __forceinline__ float mix_sample(const CrossfadeMixArgs &a, int j, float va, float vb,
                                             const float *vtab) {
     if (!a.approaching) return a.target == 0 ? va : vb;
@@ -824,12 +834,19 @@ __device__ __forceinline__ float mix_sample(const CrossfadeMixArgs &a, int j, fl
         v = a.mix_value0;
         for (long long q = 0; q < inc; ++q) v = __fadd_rn(v, a.step);
     }
-    const float PI_HALF = 3.14159265358979323846f * 0.5f;
-    const float rad = __fmul_rn(PI_HALF, v);
-    const float cs = cosf(rad);
-    const float g1 = __fmul_rn(cs, cs);
-    const float g2 = __fsub_rn(1.0f, g1);
-    return __fadd_rn(__fmul_rn(va, g1), __fmul_rn(vb, g2));
+    return mix_apply(va, vb, mix_gain(v));
+}
+
+// the same with the gain of every walk entry precomputed: gtab[k] =
+// mix_gain(mix_value0 + step + ... (k adds)); bit-identical to mix_sample
+__device__ __forceinline__ float mix_sample_g(const CrossfadeMixArgs &a, int j, float va, float vb,
+                                              const float *gtab) {
+    if (!a.approaching) return a.target == 0 ? va : vb;
+    const long long cj = a.counter0 + j + 1;
+    if (cj <= 0) return a.target == 0 ? vb : va;
+    if (a.fading >= 1 && cj >= a.fading) return a.target == 0 ? va : vb;
+    const long long inc = cj - (a.counter0 > 0 ? a.counter0 : 0);
+    return mix_apply(va, vb, gtab[inc]);
 }
 
 // the mix_value walk of one call (n + 1 entries), one thread, bit-identical
@@ -842,6 +859,8 @@ __device__ __forceinline__ void mix_walk(const CrossfadeMixArgs &a, float *vtab)
         vtab[k] = v;
     }
 }
+
+#include "la.hpp"  // (after the mix helpers: B's lookahead launch can fuse the mix)
 
 __global__ void crossfade_mix_kernel(CrossfadeMixArgs a) {
     __shared__ float vtab[1025];
@@ -1288,7 +1307,9 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         // (re-read every D steps) exceeds the Infinity Cache
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
         const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
-        auto kern = ntl ? upols_la_kernel<LOG2B, true> : upols_la_kernel<LOG2B, false>;
+        auto kern = a.la_mix == 1   ? (ntl ? upols_la_kernel<LOG2B, true, 1> : upols_la_kernel<LOG2B, false, 1>)
+                    : a.la_mix == 2 ? (ntl ? upols_la_kernel<LOG2B, true, 2> : upols_la_kernel<LOG2B, false, 2>)
+                                    : (ntl ? upols_la_kernel<LOG2B, true, 0> : upols_la_kernel<LOG2B, false, 0>);
         ProcArgs args = a;
         args.pipe = 0;
         args.lag = 0;
@@ -1304,7 +1325,9 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
         const int nstep = (channels + LS::NCH - 1) / LS::NCH;
-        hipLaunchKernelGGL(kern, dim3(args.la_nfar + args.la_nmid + nstep), dim3(LA_NT), lds, s, args);
+        if (a.la_mix == 2 && a.job[0].add0) return hipErrorInvalidValue;  // (the fused mix uses the add buffers' LDS)
+        const int xwg = a.la_mix == 1 ? LA_XWG : 0;  // A's launch: the mix_value walk workgroups
+        hipLaunchKernelGGL(kern, dim3(args.la_nfar + args.la_nmid + nstep + xwg), dim3(LA_NT), lds, s, args);
         return hipGetLastError();
     }
 }
@@ -1380,7 +1403,8 @@ hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hip
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 63); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 127); }
+bool la_fuse_mix_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_NOFMIX); }
 void set_pipeline_lag(int rows) { g_lag = rows < 0 ? -1 : rows; }
 int get_pipeline_lag() { return g_lag; }
 int get_variant() { return g_variant == VARIANT_AUTO ? -1 : g_variant; }

@@ -32,6 +32,7 @@ enum : int {
 enum : int {
     VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_NOPIPE = 4, VARIANT_NOPAIR = 8, VARIANT_NOLA = 16,
     VARIANT_LAFULL = 32,  // lookahead launches without anchors: every step sums all rows itself (tests)
+    VARIANT_NOFMIX = 64,  // crossfade on the lookahead step: stand-alone mix kernel instead of B's epilogue
     VARIANT_AUTO = 0x7fffffff
 };
 void set_variant(int v);
@@ -103,6 +104,11 @@ struct ProcArgs {
     int la_probe;          // timing probe only (wrong results): 1 = anchors idle, 2 = steps idle,
                            // 3 = far anchors only, 4 = mid anchors only
     int la_channels;       // channels of the batch (step workgroups cover LaStep::NCH each)
+    // crossfade on the lookahead step (CrossfadeConvolver::process :72-77):
+    // 1 = A's launch also writes the gains of this call's mix_value walk to mix_tab;
+    // 2 = B's launch mixes in its epilogue: out = mix(mix.buf_a, B's block)
+    int la_mix;
+    float *mix_tab;        // [n + 1] mix_gain of each mix_value walk entry (la_mix 1 writes, 2 reads)
 };
 
 struct IrArgs {
@@ -140,6 +146,7 @@ hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s);
 hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipStream_t s);
 hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStream_t s);
+bool la_fuse_mix_allowed();  // VARIANT_NOFMIX unset
 hipError_t launch_reset_state(int4 *state, int channels, hipStream_t s);
 // crossfade pair (A and B of one CrossfadeConvolver in one workgroup per channel)
 bool pair_supported(int log2b, int S);

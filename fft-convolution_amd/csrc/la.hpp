@@ -385,7 +385,7 @@ struct LaStep {
     static constexpr size_t bytes = chain_bytes > grp_bytes ? chain_bytes : grp_bytes;
 };
 
-template <int LOG2B, bool NTL, int NCH>
+template <int LOG2B, bool NTL, int NCH, int XF>
 __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, const int (&cs)[NCH],
                                         const int4 (&st)[NCH], int nvalid, unsigned char *smem) {
     using LS = LaStep<LOG2B>;
@@ -497,6 +497,12 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         dma_f32<64>(ovl, J.overlap + c * B, B);
         if (J.add0) dma_f32<64>(p0l, J.add0 + c * J.add_stride, B);
         if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
+        if constexpr (XF == 2) {
+            // crossfade, B's launch (no two-stage adds): A's block and the
+            // walk's gains (entries 1..B; entry 0 is never read) in p0l / p1l
+            dma_f32<64>(p0l, a.mix.buf_a + c * a.mix.buf_stride, B);
+            if (a.mix.approaching) dma_f32<64>(p1l, a.mix_tab + 1, B);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (NCH > 1) {
             __syncthreads();  // wave 0's twiddle table is in LDS
@@ -603,6 +609,8 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     float *p0l = ovl + B, *p1l = p0l + B;
     float *outc = J.out + c * J.out_stride;
     float *ovc = J.overlap + c * B;
+    // crossfade, B's launch: out = mix(A's block, this block) (:75-77)
+    const float *mtab = p1l - 1;  // gains of the mix_value walk, entry k at p1l[k - 1]
     bool bad = false;  // conv = pre + X (.) H[0] (:270-275), then the C2R error check
     for (int f = lane; f < F; f += 64) {
         const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
@@ -624,6 +632,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 v += p0l[j];
                 if (J.add1) v += p1l[j];
             }
+            if constexpr (XF == 2) v = mix_sample_g(a.mix, j, p0l[j], v, mtab);
             outc[j] = v;
             ovc[j] = y[B + j] * invN;  // :297-298
         }
@@ -653,8 +662,9 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 v += p0l[j];
                 if (J.add1) v += p1l[j];
             }
+            if constexpr (XF == 2) v = mix_sample_g(a.mix, j, p0l[j], v, mtab);
+            ibc[j] = inc[j];  // (before the output: a caller's output may alias its input)
             outc[j] = v;
-            ibc[j] = inc[j];
         }
         if (lane == 0) J.state[c] = make_int4(cur, act, 0, keep | FLAG_INBUF | tag);
     }
@@ -663,7 +673,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
 // a channel off the lookahead path (partial block, buffered input, short
 // response) in the workgroup: its channels run one at a time, out of line
 // (the rare fallback keeps its registers out of the step's allocation)
-template <int LOG2B, bool NTL>
+template <int LOG2B, bool NTL, int XF>
 __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0, int nvalid, unsigned char *smem) {
     const ProcArgs &a = *ap;
     const ProcJob &J = a.job[0];
@@ -674,7 +684,21 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
         if (la_eligible<LOG2B>(st, J.n)) {
             const int c1[1] = {c};
             const int4 s1[1] = {st};
-            la_step<LOG2B, NTL, 1>(a, J, c1, s1, 1, smem);
+            la_step<LOG2B, NTL, 1, XF>(a, J, c1, s1, 1, smem);
+        } else if (XF == 2) {
+            // crossfade, B's launch: the generic step writes B's block to
+            // buf_b, then the workgroup mixes it with A's (same-workgroup
+            // global writes are visible after the barrier)
+            ProcJob Jb = J;
+            Jb.out = const_cast<float *>(a.mix.buf_b);
+            Jb.out_stride = a.mix.buf_stride;
+            process_job<LOG2B, LA_NT, false, NTL>(a, Jb, (size_t)c, st, smem);
+            __syncthreads();
+            const float *ya = a.mix.buf_a + (size_t)c * a.mix.buf_stride;
+            const float *yb = a.mix.buf_b + (size_t)c * a.mix.buf_stride;
+            float *o = J.out + (size_t)c * J.out_stride;
+            const float *mtab = a.mix_tab;
+            for (int j = threadIdx.x; j < J.n; j += LA_NT) o[j] = mix_sample_g(a.mix, j, ya[j], yb[j], mtab);
         } else {
             process_job<LOG2B, LA_NT, false, NTL>(a, J, (size_t)c, st, smem);
         }
@@ -682,14 +706,51 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
 }
 
 // grid: [far anchors | mid anchors | step workgroups] (or the steps first)
-template <int LOG2B, bool NTL>
+constexpr int LA_XWG = 8;  // A's launch: leading workgroups (the first writes the mix_value walk)
+
+// crossfade, A's launch: this call's mix_value walk (the reference's
+// sequential f32 additions, one lane, into LDS), then its gains, to mix_tab for B's
+// launch (out of line: keeps its registers out of the step's allocation)
+__device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsigned char *smem) {
+    if (!ap->mix.approaching) return;
+    // (the walk's operands in registers: stores through the LDS pointer could
+    // otherwise alias the kernel arguments and reload them every entry)
+    const int n = ap->mix.n;
+    const float step = ap->mix.step;
+    float *mt = ap->mix_tab;
+    float *t = reinterpret_cast<float *>(smem);
+    if (threadIdx.x == 0) {
+        float v = ap->mix.mix_value0;
+        t[0] = v;
+        for (int k = 1; k <= n; ++k) {  // mix_value += step (:259), one f32 rounding each
+            v = __fadd_rn(v, step);
+            t[k] = v;
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k <= n; k += LA_NT) mt[k] = mix_gain(t[k]);  // gains, in parallel
+}
+
+// XF: crossfade role of the launch (ProcArgs::la_mix): 0 none; 1 = A's launch,
+// whose first workgroup also writes the gains of this call's mix_value walk to mix_tab;
+// 2 = B's launch, whose steps mix A's block with their own
+template <int LOG2B, bool NTL, int XF>
 __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
     using LS = LaStep<LOG2B>;
     constexpr int NCH = LS::NCH;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if constexpr (XF == 1) {
+        // 8 extra workgroups at the front of the grid (one per XCD: the far
+        // anchors' XCD placement behind them is unchanged); the first walks,
+        // so the walk starts with the launch and runs beside the steps
+        if (blockIdx.x < LA_XWG) {
+            if (blockIdx.x == 0) la_mix_walk((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), smem);
+            return;
+        }
+    }
     const int nanchor = a.la_nfar + a.la_nmid;
-    const int nstep = (int)gridDim.x - nanchor;  // step workgroups
-    const int b = blockIdx.x;
+    const int nstep = (int)gridDim.x - nanchor - (XF == 1 ? LA_XWG : 0);  // step workgroups
+    const int b = (int)blockIdx.x - (XF == 1 ? LA_XWG : 0);
     const int ba = a.la_steps_first ? b - nstep : b;  // anchor index, < 0 for a step
     if (ba >= 0 && ba < nanchor) {
         if (a.la_probe != 1 && a.la_probe != 6) {
@@ -718,7 +779,7 @@ __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
         all &= k >= nvalid || la_eligible<LOG2B>(st[k], J.n);
     }
     if (all)
-        la_step<LOG2B, NTL, NCH>(a, J, cs, st, nvalid, smem);
+        la_step<LOG2B, NTL, NCH, XF>(a, J, cs, st, nvalid, smem);
     else  // (the arguments by their kernarg address: no private copy of the block)
-        la_fallback<LOG2B, NTL>((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), c0, nvalid, smem);
+        la_fallback<LOG2B, NTL, XF>((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), c0, nvalid, smem);
 }

@@ -14,7 +14,7 @@ from common import assert_close, ir, white
 
 pytestmark = pytest.mark.gpu
 
-NOLA, LAFULL = 16, 32
+NOLA, LAFULL, NOFMIX = 16, 32, 64
 
 
 def _refs(oracle_mod, hs, B, L):
@@ -211,3 +211,49 @@ def test_lookahead_crossfade_vs_oracle(amd, oracle_mod, B, L):
     for c in range(C):
         assert_close(outs[-1][c], exp[c], what=f"lookahead ch {c}")
         assert_close(outs[NOLA][c], exp[c], what=f"full-sum ch {c}")
+
+
+@pytest.mark.parametrize("B,L", [(256, 40 * 256 + 5), (512, 44 * 512)])
+def test_lookahead_crossfade_fused_mix(amd, oracle_mod, B, L):
+    """The crossfade mix (src/crossfade_convolver.rs:75-77, Crossfader::mix
+    :242-278) fused into B's lookahead launch -- A's launch walks mix_value into
+    a table, B's epilogue mixes -- is bit-identical to the stand-alone mix
+    kernel (VARIANT_NOFMIX): through fades, holds, pending swaps, a short
+    output (out_len < B: stand-alone mix), and a NaN block (C2R error, then the
+    buffered channel's generic step inside the fused launch)."""
+    rng = np.random.default_rng(410 + B)
+    C = 4
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    blocks = 64
+    ups = {3: L, 9: L - B, 20: L, 41: L - 2 * B}
+    xs = [np.stack([white(rng, B) for _ in range(C)]) for _ in range(blocks)]
+    for j in (44, 45):
+        xs[j][2, 17] = np.nan
+    news = {i: np.stack([ir(rng, n) for _ in range(C)]) for i, n in ups.items()}
+    olen = {i: (B if i % 11 != 7 else B // 2) for i in range(blocks)}
+    outs = {}
+    for v in (-1, NOFMIX):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.CrossfadeConvolver.init(hs, B, L, channels=C)
+            ys = []
+            for i in range(blocks):
+                if i in news:
+                    conv.update(news[i])
+                ys.append(conv.process(xs[i], olen[i]))
+            outs[v] = np.concatenate(ys, axis=1)
+        finally:
+            amd.set_kernel_variant(-1)
+    assert np.array_equal(outs[-1], outs[NOFMIX], equal_nan=True)
+    refs = [oracle_mod.CrossfadeConvolver.init(hs[c], B, L) for c in range(C)]
+    exp = []
+    for i in range(blocks):
+        if i in news:
+            for c in range(C):
+                refs[c].update(news[i][c])
+        exp.append(np.stack([refs[c].process(xs[i][c], olen[i]) for c in range(C)]))
+    exp = np.concatenate(exp, axis=1)
+    for c in range(C):
+        m = ~np.isnan(exp[c])
+        assert np.array_equal(np.isnan(outs[-1][c]), ~m), c
+        assert_close(outs[-1][c][m], exp[c][m], what=f"fused ch {c}")
