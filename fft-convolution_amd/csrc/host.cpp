@@ -1001,7 +1001,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 127) return fail(FFTCONV_E_INVALID, "variant must be 0..127 (or -1 = auto)");
+    if (variant > 255) return fail(FFTCONV_E_INVALID, "variant must be 0..255 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }

@@ -1118,6 +1118,62 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
     for (int m = tid; m < B; m += NT) row[m] = real_post<LOG2B, NT>(Z, m, a.tw);
 }
 
+// The same transforms one segment per wave (64 <= B <= 1024): the twiddle
+// table is staged in LDS once per workgroup, the stages synchronise at wave
+// level, and each wave walks IR_SPW segments.  Same butterflies in the same
+// order as ir_segments_kernel, so the same bits.
+// grid (ceil(S / (4 * IR_SPW)), channels); LDS: tw (2B) | 4 x (bufA | bufB)
+constexpr int IR_SPW = 2;
+template <int LOG2B>
+__global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
+    constexpr int B = 1 << LOG2B;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *twl = reinterpret_cast<float2 *>(smem);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    float2 *bufA = twl + 2 * B + (size_t)wave * 2 * B;
+    float2 *bufB = bufA + B;
+    const size_t c = a.chan0 + blockIdx.y;
+    const size_t rows = (size_t)a.S * B;
+    const long long active = (a.len_active + B - 1) / B;
+    dma_16b<256>(twl, a.tw, 2 * B * (int)sizeof(float2));
+    if (a.update_state && blockIdx.x == 0) {
+        // update(): zero overlap / pre_multiplied / conv, set active (:199-204)
+        for (int j = tid; j < B; j += 256) {
+            a.overlap[c * B + j] = 0.f;
+            a.pre[c * B + j] = make_float2(0.f, 0.f);
+        }
+        if (tid == 0) {
+            a.state[c].y = (int)active;
+            a.state[c].w &= ~(FLAG_PRE | LA_MASK | SEQ_MASK);  // the stored pre / window used the old response
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const float *src = a.src + blockIdx.y * a.src_stride;
+    for (int q = 0; q < IR_SPW; ++q) {
+        const int i = (blockIdx.x * 4 + wave) * IR_SPW + q;
+        if (i >= a.S) break;
+        float2 *row = a.H + c * rows + (size_t)i * B;
+        if (i >= active) {  // :224-226
+            for (int m = lane; m < B; m += 64) row[m] = make_float2(0.f, 0.f);
+            continue;
+        }
+        const long long base = (long long)i * B;
+        for (int m = lane; m < B; m += 64) {
+            const long long i0 = base + 2 * m, i1 = base + 2 * m + 1;
+            float2 z;
+            z.x = (2 * m < B && i0 < a.len_data) ? src[i0] : 0.f;
+            z.y = (2 * m + 1 < B && i1 < a.len_data) ? src[i1] : 0.f;
+            bufA[m] = z;
+        }
+        wave_sync();
+        const float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);
+        for (int m = lane; m < B; m += 64) row[m] = real_post<LOG2B, 64>(Z, m, twl);
+        wave_sync();  // (the next segment overwrites both buffers)
+    }
+}
+
 // ---------------------------------------------------------------------------
 // TwoStage sub-chunk (src/fft_convolver.rs:452-475): output += precalculated0
 // then += precalculated (two passes, like the reference), and append the
@@ -1222,6 +1278,18 @@ static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t 
 
 template <int LOG2B>
 static hipError_t launch_ir_t(const IrArgs &a, int channels, hipStream_t s) {
+    if constexpr (LOG2B >= 6 && LOG2B <= 10) {
+        if (g_variant == VARIANT_AUTO || !(g_variant & VARIANT_IRBLOCK)) {
+            constexpr size_t lds = 10 * (size_t)(1 << LOG2B) * sizeof(float2);  // tw + 4 waves x 2 buffers
+            auto kern = ir_segments_wave_kernel<LOG2B>;
+            if (lds > 64 * 1024) {
+                hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(kern, dim3((a.S + 4 * IR_SPW - 1) / (4 * IR_SPW), channels), dim3(256), lds, s, a);
+            return hipGetLastError();
+        }
+    }
     constexpr size_t lds = 2 * (size_t)(1 << LOG2B) * sizeof(float2) + 16;
     auto kern = ir_segments_kernel<LOG2B, kNT>;
     if (lds > 64 * 1024) {
@@ -1403,7 +1471,7 @@ hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hip
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 127); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 255); }
 bool la_fuse_mix_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_NOFMIX); }
 void set_pipeline_lag(int rows) { g_lag = rows < 0 ? -1 : rows; }
 int get_pipeline_lag() { return g_lag; }

@@ -33,6 +33,7 @@ enum : int {
     VARIANT_ZIGZAG = 1, VARIANT_NT = 2, VARIANT_NOPIPE = 4, VARIANT_NOPAIR = 8, VARIANT_NOLA = 16,
     VARIANT_LAFULL = 32,  // lookahead launches without anchors: every step sums all rows itself (tests)
     VARIANT_NOFMIX = 64,  // crossfade on the lookahead step: stand-alone mix kernel instead of B's epilogue
+    VARIANT_IRBLOCK = 128,  // IR transforms: one segment per workgroup (else one per wave, 64 <= B <= 1024)
     VARIANT_AUTO = 0x7fffffff
 };
 void set_variant(int v);

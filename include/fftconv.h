@@ -74,7 +74,9 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
  * (every full block sums all its FDL rows itself; bit-identical to the
  * lookahead path, for tests), bit 6 = crossfade on the lookahead step with
  * the stand-alone mix kernel (by default B's launch mixes in its epilogue,
- * from gains A's launch precomputed; bit-identical either way).
+ * from gains A's launch precomputed; bit-identical either way), bit 7 = IR
+ * transforms (init / update) one segment per workgroup (by default one per
+ * wave for 64 <= B <= 1024; bit-identical).
  * Lookahead (automatic for standalone FFTConvolver batches with
  * 128 <= B <= 512 and >= 27 segments): the far FDL rows' terms of the next
  * 8 full blocks are summed ahead in one pass over H and the FDL, so a

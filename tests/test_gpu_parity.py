@@ -660,3 +660,38 @@ def test_cfg2_full_size_sampled_channels(amd, oracle_mod):
         conv2.process_device(x2d.data_ptr() + 4 * s * B, steps * B, y2d.data_ptr() + 4 * s * B, steps * B, B, stream)
     torch.cuda.synchronize()
     assert torch.equal(y2d, 2.0 * yd)
+
+
+@pytest.mark.parametrize("B,L", [(64, 5000), (256, 40 * 256 + 5), (512, 44 * 512 - 3), (1024, 9 * 1024 + 17)])
+def test_ir_transform_wave_kernel_bitwise(amd, oracle_mod, B, L):
+    """FFTConvolver::init / update (src/fft_convolver.rs:145-156, :204-226): the
+    IR segment transforms one per wave (default, 64 <= B <= 1024) give the same
+    spectra bits as one per workgroup (variant bit 7), through init, an update
+    to a shorter response (zeroed rows) and back; and match the oracle."""
+    rng = np.random.default_rng(700 + B)
+    C = 3
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    news = {4: np.stack([ir(rng, L // 3) for _ in range(C)]), 9: np.stack([ir(rng, L) for _ in range(C)])}
+    xs = [np.stack([white(rng, B) for _ in range(C)]) for _ in range(14)]
+    outs = []
+    for v in (16, 16 | 128):  # same step kernels (16: full-sum step); 128: IR transforms per workgroup
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+            ys = []
+            for i, x in enumerate(xs):
+                if i in news:
+                    conv.update(news[i])
+                ys.append(conv.process(x))
+            outs.append(np.concatenate(ys, axis=1))
+        finally:
+            amd.set_kernel_variant(-1)
+    assert np.array_equal(outs[0], outs[1])
+    for c in range(C):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        exp = []
+        for i, x in enumerate(xs):
+            if i in news:
+                ref.update(news[i][c])
+            exp.append(ref.process(x[c]))
+        assert_close(outs[0][c], np.concatenate(exp), what=f"ch {c}")
