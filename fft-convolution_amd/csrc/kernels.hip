@@ -837,16 +837,21 @@ __device__ __forceinline__ float mix_sample(const CrossfadeMixArgs &a, int j, fl
     return mix_apply(va, vb, mix_gain(v));
 }
 
-// the same with the gain of every walk entry precomputed: gtab[k] =
-// mix_gain(mix_value0 + step + ... (k adds)); bit-identical to mix_sample
-__device__ __forceinline__ float mix_sample_g(const CrossfadeMixArgs &a, int j, float va, float vb,
-                                              const float *gtab) {
-    if (!a.approaching) return a.target == 0 ? va : vb;
+// Crossfader::mix for sample j as a selector word: MIX_SEL_A / MIX_SEL_B take
+// that convolver's sample as is (hold, snap, not fading), anything else is the
+// gain g1 in [0, 1] of the blend.  mix_select(va, vb, mix_selector(...)) is
+// bit-identical to mix_sample.
+constexpr float MIX_SEL_A = 2.0f, MIX_SEL_B = 3.0f;
+__device__ __forceinline__ float mix_selector(const CrossfadeMixArgs &a, int j, const float *vtab) {
+    const float sa = a.target == 0 ? MIX_SEL_A : MIX_SEL_B, sb = a.target == 0 ? MIX_SEL_B : MIX_SEL_A;
+    if (!a.approaching) return sa;
     const long long cj = a.counter0 + j + 1;
-    if (cj <= 0) return a.target == 0 ? vb : va;
-    if (a.fading >= 1 && cj >= a.fading) return a.target == 0 ? va : vb;
-    const long long inc = cj - (a.counter0 > 0 ? a.counter0 : 0);
-    return mix_apply(va, vb, gtab[inc]);
+    if (cj <= 0) return sb;                            // hold the previous target
+    if (a.fading >= 1 && cj >= a.fading) return sa;    // reached (snap)
+    return mix_gain(vtab[cj - (a.counter0 > 0 ? a.counter0 : 0)]);
+}
+__device__ __forceinline__ float mix_select(float va, float vb, float sel) {
+    return sel == MIX_SEL_A ? va : (sel == MIX_SEL_B ? vb : mix_apply(va, vb, sel));
 }
 
 // the mix_value walk of one call (n + 1 entries), one thread, bit-identical

@@ -106,10 +106,10 @@ struct ProcArgs {
                            // 3 = far anchors only, 4 = mid anchors only
     int la_channels;       // channels of the batch (step workgroups cover LaStep::NCH each)
     // crossfade on the lookahead step (CrossfadeConvolver::process :72-77):
-    // 1 = A's launch also writes the gains of this call's mix_value walk to mix_tab;
+    // 1 = A's launch also writes this call's per-sample mix selectors to mix_tab;
     // 2 = B's launch mixes in its epilogue: out = mix(mix.buf_a, B's block)
     int la_mix;
-    float *mix_tab;        // [n + 1] mix_gain of each mix_value walk entry (la_mix 1 writes, 2 reads)
+    float *mix_tab;        // [n] mix_selector of each sample (la_mix 1 writes, 2 reads)
 };
 
 struct IrArgs {

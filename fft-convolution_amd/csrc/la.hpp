@@ -499,9 +499,9 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
         if constexpr (XF == 2) {
             // crossfade, B's launch (no two-stage adds): A's block and the
-            // walk's gains (entries 1..B; entry 0 is never read) in p0l / p1l
+            // per-sample mix selectors (la_mix_walk) in p0l / p1l
             dma_f32<64>(p0l, a.mix.buf_a + c * a.mix.buf_stride, B);
-            if (a.mix.approaching) dma_f32<64>(p1l, a.mix_tab + 1, B);
+            dma_f32<64>(p1l, a.mix_tab, B);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (NCH > 1) {
@@ -610,7 +610,6 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     float *outc = J.out + c * J.out_stride;
     float *ovc = J.overlap + c * B;
     // crossfade, B's launch: out = mix(A's block, this block) (:75-77)
-    const float *mtab = p1l - 1;  // gains of the mix_value walk, entry k at p1l[k - 1]
     bool bad = false;  // conv = pre + X (.) H[0] (:270-275), then the C2R error check
     for (int f = lane; f < F; f += 64) {
         const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
@@ -632,7 +631,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 v += p0l[j];
                 if (J.add1) v += p1l[j];
             }
-            if constexpr (XF == 2) v = mix_sample_g(a.mix, j, p0l[j], v, mtab);
+            if constexpr (XF == 2) v = mix_select(p0l[j], v, p1l[j]);
             outc[j] = v;
             ovc[j] = y[B + j] * invN;  // :297-298
         }
@@ -662,7 +661,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 v += p0l[j];
                 if (J.add1) v += p1l[j];
             }
-            if constexpr (XF == 2) v = mix_sample_g(a.mix, j, p0l[j], v, mtab);
+            if constexpr (XF == 2) v = mix_select(p0l[j], v, p1l[j]);
             ibc[j] = inc[j];  // (before the output: a caller's output may alias its input)
             outc[j] = v;
         }
@@ -697,8 +696,8 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
             const float *ya = a.mix.buf_a + (size_t)c * a.mix.buf_stride;
             const float *yb = a.mix.buf_b + (size_t)c * a.mix.buf_stride;
             float *o = J.out + (size_t)c * J.out_stride;
-            const float *mtab = a.mix_tab;
-            for (int j = threadIdx.x; j < J.n; j += LA_NT) o[j] = mix_sample_g(a.mix, j, ya[j], yb[j], mtab);
+            const float *sel = a.mix_tab;
+            for (int j = threadIdx.x; j < J.n; j += LA_NT) o[j] = mix_select(ya[j], yb[j], sel[j]);
         } else {
             process_job<LOG2B, LA_NT, false, NTL>(a, J, (size_t)c, st, smem);
         }
@@ -708,27 +707,30 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
 // grid: [far anchors | mid anchors | step workgroups] (or the steps first)
 constexpr int LA_XWG = 8;  // A's launch: leading workgroups (the first writes the mix_value walk)
 
-// crossfade, A's launch: this call's mix_value walk (the reference's
-// sequential f32 additions, one lane, into LDS), then its gains, to mix_tab for B's
-// launch (out of line: keeps its registers out of the step's allocation)
+// crossfade, A's launch: per-sample mix selectors of this call for B's
+// launch (mix_select): Crossfader::mix (:242-278) for sample j is A's sample,
+// B's sample, or the raised-cosine blend with gain g1 of the mix_value walk
+// entry it has reached -- the reference's sequential f32 additions, one lane,
+// into LDS -- so B's epilogue reads one word per sample and no crossfader
+// state.  (Out of line: keeps its registers out of the step's allocation.)
 __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsigned char *smem) {
-    if (!ap->mix.approaching) return;
     // (the walk's operands in registers: stores through the LDS pointer could
     // otherwise alias the kernel arguments and reload them every entry)
-    const int n = ap->mix.n;
-    const float step = ap->mix.step;
+    const CrossfadeMixArgs m = ap->mix;
     float *mt = ap->mix_tab;
     float *t = reinterpret_cast<float *>(smem);
-    if (threadIdx.x == 0) {
-        float v = ap->mix.mix_value0;
-        t[0] = v;
-        for (int k = 1; k <= n; ++k) {  // mix_value += step (:259), one f32 rounding each
-            v = __fadd_rn(v, step);
-            t[k] = v;
+    if (m.approaching) {
+        if (threadIdx.x == 0) {
+            float v = m.mix_value0;
+            t[0] = v;
+            for (int k = 1; k <= m.n; ++k) {  // mix_value += step (:259), one f32 rounding each
+                v = __fadd_rn(v, m.step);
+                t[k] = v;
+            }
         }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int k = threadIdx.x; k <= n; k += LA_NT) mt[k] = mix_gain(t[k]);  // gains, in parallel
+    for (int j = threadIdx.x; j < m.n; j += LA_NT) mt[j] = mix_selector(m, j, t);
 }
 
 // XF: crossfade role of the launch (ProcArgs::la_mix): 0 none; 1 = A's launch,
