@@ -58,3 +58,21 @@ def test_no_cpu_fallback_without_device():
         fftconv_amd.TwoStageFFTConvolver.init(np.ones(8, np.float32), 4, 8)
     with pytest.raises(fftconv_amd.DeviceError):
         fftconv_amd.CrossfadeConvolver.init(np.ones(8, np.float32), 4, 8)
+
+
+def test_kernel_variant_knob_range():
+    """fftconv_set_kernel_variant (include/fftconv.h): -1 (automatic) and
+    0..255 are accepted (bits 0-7), anything above is FFTCONV_E_INVALID; a
+    host-only setter, no device needed."""
+    import fftconv_amd
+
+    try:
+        for v in (0, 64, 128, 255):
+            fftconv_amd.set_kernel_variant(v)
+            assert fftconv_amd.get_kernel_variant() == v
+        with pytest.raises(fftconv_amd.ConvolutionPanic):
+            fftconv_amd.set_kernel_variant(256)
+        assert fftconv_amd.get_kernel_variant() == 255
+    finally:
+        fftconv_amd.set_kernel_variant(-1)
+    assert fftconv_amd.get_kernel_variant() == -1

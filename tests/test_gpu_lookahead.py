@@ -213,7 +213,7 @@ def test_lookahead_crossfade_vs_oracle(amd, oracle_mod, B, L):
         assert_close(outs[NOLA][c], exp[c], what=f"full-sum ch {c}")
 
 
-@pytest.mark.parametrize("B,L", [(256, 40 * 256 + 5), (512, 44 * 512)])
+@pytest.mark.parametrize("B,L", [(128, 45 * 128 - 7), (256, 40 * 256 + 5), (512, 44 * 512)])
 def test_lookahead_crossfade_fused_mix(amd, oracle_mod, B, L):
     """The crossfade mix (src/crossfade_convolver.rs:75-77, Crossfader::mix
     :242-278) fused into B's lookahead launch -- A's launch walks mix_value into
