@@ -4,14 +4,17 @@
 Workload (BASELINE.json configs[1], the north-star metric's config): 1024
 channels per GPU, block 256, a distinct 48,000-tap white-noise IR per channel,
 f32.  One *step* = one FFTConvolver::process call of 256 samples on every
-channel (src/fft_convolver.rs:229-309) = one fused kernel launch: forward R2C
+channel (src/fft_convolver.rs:215-295) = one fused kernel launch: forward R2C
 of the new block into the FDL, the S-segment spectral MAC, C2R and overlap-add
--- with the lookahead step (csrc/la.hpp) the FDL rows beyond the 4 nearest are
-summed ahead by the launch's anchor workgroups (rows 5..32 four blocks ahead
-for C/4 channels, rows >= 33 thirty-two blocks ahead for C/32 channels).
+-- with the lookahead step (csrc/la.hpp) each step sums only the 5 nearest
+FDL rows itself; rows 6..32 are summed 5 blocks ahead by mid anchors (C/5
+channels per launch) and rows >= 33 thirty-two blocks ahead by far anchors
+(C/32 channels per launch), S >= 40.  The timed steps are submitted through
+process_device_steps (the C ABI loops over the calls), not one Python call each.
 Inputs are resident in HBM when the timed region starts.
 
-Multi-GPU (BASELINE configs[3], 8192 channels on 8 GPUs): one process per GPU,
+Multi-GPU (BASELINE configs[3], 8192 channels on 8 GPUs): one process per GPU
+(`--gpus N` without a launcher spawns the N rank processes itself),
 1024 channels per rank (weak scaling, channel shards have no data-path
 exchange); barrier + synchronize around the timed region, max time over ranks.
 `--dry shared` instead broadcasts one dry block per step from rank 0 over RCCL
@@ -88,7 +91,41 @@ def parse():
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     p.add_argument("--same-device", action="store_true",
                    help="debug: every rank on device 0 (rehearse the N>1 path on a one-GPU box, gloo)")
+    p.add_argument("--per-call", action="store_true",
+                   help="submit one process_device call per step from Python (default: process_device_steps)")
+    p.add_argument("--spawn-probe", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
+
+
+def free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N fresh rank processes,
+    one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set -- the
+    environment torch.distributed.run would give them -- before this process
+    touches the GPU, and wait for all of them.  Rank 0 prints the JSON line.
+    Returns the first non-zero exit status (0 if every rank succeeded), so no
+    path can report N ranks' throughput from one process."""
+    port = free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"bench.py: rank exit statuses {rcs}", file=sys.stderr)
+        return bad[0]
+    return 0
 
 
 def pmc_traffic(args):
@@ -180,8 +217,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus and world > 1:
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(spawn_ranks(args))
+    if world != args.gpus:
+        # a launcher's world size wins: the job runs (and reports) that many ranks
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; running {world} rank(s)", file=sys.stderr)
         args.gpus = world
+    if args.spawn_probe:  # (tests: the rank environment, no GPU work)
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world}), flush=True)
+        return
     traffic, traffic_note = None, "not collected (N>1 or --pmc off)"
     if args.pmc == "auto" and world == 1 and not args.pmc_inner:
         traffic, traffic_note = pmc_traffic(args)  # child processes, before this one touches the GPU
@@ -190,6 +234,9 @@ def main():
 
     if args.same_device:
         local_rank = 0
+    elif local_rank >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} needs device {local_rank}, "
+                         f"{torch.cuda.device_count()} visible (one process per GPU)")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
@@ -238,8 +285,22 @@ def main():
         else:
             conv.process_device(xin[r].data_ptr(), B, yout[r].data_ptr(), B, B, sh)
 
-    for i in range(args.warmup):
-        step(i)
+    def steps(i0: int, k: int):
+        """k consecutive steps from step i0: one process_device_steps call per
+        run of ring slots (the ABI loops over the calls in C++, so Python's
+        per-call submission cost stays out of the timed region)."""
+        if args.per_call or args.dry == "shared":
+            for i in range(i0, i0 + k):
+                step(i)
+            return
+        i = i0
+        while i < i0 + k:
+            r = i % ring
+            n = min(ring - r, i0 + k - i)
+            conv.process_device_steps(xin[r].data_ptr(), B, C * B, yout[r].data_ptr(), B, C * B, B, n, sh)
+            i += n
+
+    steps(0, args.warmup)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -249,8 +310,7 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for i in range(args.steps):
-        step(args.warmup + i)
+    steps(args.warmup, args.steps)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist is not None:
@@ -267,7 +327,7 @@ def main():
     if not torch.isfinite(yout).all():
         raise SystemExit("non-finite output")
 
-    total_samples = args.gpus * C * B * args.steps
+    total_samples = world * C * B * args.steps  # the ranks that actually ran
     value = total_samples / elapsed / 1e6
     per_launch_s = kern_ms / 1000.0 / args.steps
     canonical_bytes = algorithmic_bytes_per_channel_block(B, L) * C
@@ -285,13 +345,14 @@ def main():
         return
     if rank == 0:
         cpu = None
-        if args.gpus == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(C, B, L, args.cpu_seconds)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "MSamples/s",
-            "n_gpus": args.gpus,
+            # distinct devices: --same-device rehearsals share one GPU
+            "n_gpus": 1 if args.same_device else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1000.0 / args.steps, 5),
@@ -302,14 +363,15 @@ def main():
             "data": "synthetic: white-noise U[-1,1) dry blocks resident in HBM, distinct white-noise IR "
                     "U[-1,1)/sqrt(L) per channel",
             "config": {
-                "workload": "cfg2 FFTConvolver batch" if args.gpus == 1 else "cfg4 FFTConvolver channel shards",
+                "workload": "cfg2 FFTConvolver batch" if world == 1 else "cfg4 FFTConvolver channel shards",
                 "channels_per_gpu": C,
-                "channels_total": C * args.gpus,
+                "channels_total": C * world,
                 "block_size": B,
                 "ir_len": L,
                 "segments": S,
                 "dry_input": args.dry,
-                "parallelism": f"channel-shard x{args.gpus}",
+                "parallelism": f"channel-shard x{world}",
+                "submission": "per-call" if args.per_call or args.dry == "shared" else "process_device_steps",
             },
             "roofline": {
                 "bound": "hbm",
@@ -330,6 +392,8 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if args.same_device:
+            line["same_device"] = True  # a rehearsal: every rank on device 0, not an N-GPU result
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -1,6 +1,6 @@
 // fft_lds.hpp -- workgroup-cooperative real FFT of length N = 2B on gfx950.
 //
-// Replaces the reference's Fft wrapper (src/fft_convolver.rs:15-64), which
+// Replaces the reference's Fft wrapper (src/fft_convolver.rs:1-50), which
 // delegates to realfft/rustfft on the CPU.  The transform is the same
 // algorithm realfft publishes for even lengths: pack the N real samples as
 // M = N/2 complex points z[n] = x[2n] + i x[2n+1], run an M-point complex

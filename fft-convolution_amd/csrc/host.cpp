@@ -2,8 +2,8 @@
 //
 // The three reference types are mirrored as batches of device-resident
 // channels:
-//   UniformCore   <- FFTConvolver          (src/fft_convolver.rs:100-321)
-//   TwoStageCore  <- TwoStageFFTConvolver  (src/fft_convolver.rs:337-526)
+//   UniformCore   <- FFTConvolver          (src/fft_convolver.rs:86-307)
+//   TwoStageCore  <- TwoStageFFTConvolver  (src/fft_convolver.rs:323-512)
 //   CrossfadeCore <- CrossfadeConvolver<FFTConvolver> (src/crossfade_convolver.rs:3-105)
 // Per-channel block state lives on the device (the fused kernel advances it);
 // the host only keeps what the reference keeps per *instance* and what all
@@ -155,11 +155,11 @@ struct UniformCore {
         device = dev;
         C = channels;
         ir_len = max_len;
-        B = next_pow2(max_block_size);                             // :129
+        B = next_pow2(max_block_size);                             // :115
         log2b = ilog2(B);
         if (log2b > kMaxLog2Block)
             return fail(FFTCONV_E_UNSUPPORTED, "block size " + std::to_string(B) + " exceeds 8192");
-        S = ceil_div(ir_len, B);                                   // :131
+        S = ceil_div(ir_len, B);                                   // :117
         if (S * B > (size_t)INT32_MAX || C > (size_t)INT32_MAX)
             return fail(FFTCONV_E_UNSUPPORTED, "geometry exceeds 32-bit indexing");
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -228,7 +228,7 @@ struct UniformCore {
 
     int init(int dev, size_t channels, const float *responses, size_t len, size_t stride, size_t max_block,
              size_t max_len) {
-        if (max_len < len)                                          // :120-124
+        if (max_len < len)                                          // :106-110
             return fail(FFTCONV_E_INVALID,
                         "max_response_length must be at least the length of the initial impulse response");
         if (int r = check_device(dev)) return r;
@@ -245,10 +245,10 @@ struct UniformCore {
         return FFTCONV_OK;
     }
 
-    // FFTConvolver::update (:188-227) for channels [chan0, chan0+nch)
+    // FFTConvolver::update (:174-213) for channels [chan0, chan0+nch)
     int update_host(size_t chan0, size_t nch, const float *src, size_t len, size_t stride) {
         if (len > ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
-        if (ir_len == 0) return FFTCONV_OK;                        // :195-197
+        if (ir_len == 0) return FFTCONV_OK;                        // :181-183
         DeviceGuard g(device);
         HIP_TRY(hipDeviceSynchronize());  // work may be in flight on a caller stream
         if (int r = upload(chan0, nch, src, len, stride, stream)) return r;
@@ -265,7 +265,7 @@ struct UniformCore {
         return ir_from_device(0, C, src, stride, len, len, true, s);
     }
 
-    int reset(hipStream_t s) {  // :310-320
+    int reset(hipStream_t s) {  // :296-306
         if (X.n) HIP_TRY(hipMemsetAsync(X.p, 0, X.bytes(), s));
         if (overlap.n) HIP_TRY(hipMemsetAsync(overlap.p, 0, overlap.bytes(), s));
         if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), s));
@@ -380,7 +380,7 @@ struct UniformCore {
 };
 
 // ---------------------------------------------------------------------------
-// TwoStageCore -- TwoStageFFTConvolver (src/fft_convolver.rs:337-526)
+// TwoStageCore -- TwoStageFFTConvolver (src/fft_convolver.rs:323-512)
 // ---------------------------------------------------------------------------
 struct TwoStageCore {
     int device = 0;
@@ -395,7 +395,7 @@ struct TwoStageCore {
     hipStream_t stream = nullptr;
     // The T-sized tail convolution runs on its own stream: its result is first
     // read one whole tail period later (after the next swap), which is the
-    // reference's "might be done in some background thread" (:492).
+    // reference's "might be done in some background thread" (:478).
     hipStream_t side = nullptr;
     hipEvent_t ev_main = nullptr, ev_tail = nullptr;
     bool tail_in_flight = false;
@@ -458,9 +458,9 @@ struct TwoStageCore {
 
     int init(int dev, size_t channels, const float *responses, size_t len, size_t stride, size_t block_size,
              size_t max_len) {
-        head_bs = block_size;                                                   // :355
-        T = fftconv_compute_tail_block_size(block_size, max_len);              // :356
-        if (max_len < len)                                                      // :358-362
+        head_bs = block_size;                                                   // :341
+        T = fftconv_compute_tail_block_size(block_size, max_len);              // :342
+        if (max_len < len)                                                      // :344-348
             return fail(FFTCONV_E_INVALID,
                         "max_response_length must be at least the length of the initial impulse response");
         if (int r = check_device(dev)) return r;
@@ -470,7 +470,7 @@ struct TwoStageCore {
         C = channels;
         DeviceGuard g(dev);
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        // padded_ir = response zero-extended to max_len (:363-364); sub-ranges
+        // padded_ir = response zero-extended to max_len (:349-350); sub-ranges
         // are cut on the host so each stage sees exactly its reference slice
         const size_t sstride = stride == 0 ? 0 : stride;
         auto slice = [&](size_t off, size_t cnt, std::vector<float> &buf) -> size_t {
@@ -484,19 +484,19 @@ struct TwoStageCore {
             return sstride == 0 ? 0 : cnt;
         };
         std::vector<float> tmp;
-        const size_t head_ir_len = std::min(max_len, T);                        // :366-368
+        const size_t head_ir_len = std::min(max_len, T);                        // :352-354
         head.reset(new (std::nothrow) UniformCore());
         if (!head) return fail(FFTCONV_E_NOMEM, "out of host memory");
         size_t st = slice(0, head_ir_len, tmp);
         if (int r = head->init(dev, C, tmp.data(), head_ir_len, st, head_bs, head_ir_len)) return r;
-        if (max_len > T) {                                                      // :370-382
+        if (max_len > T) {                                                      // :356-368
             const size_t tl = std::min(max_len - T, T);
             tail0.reset(new (std::nothrow) UniformCore());
             if (!tail0) return fail(FFTCONV_E_NOMEM, "out of host memory");
             st = slice(T, tl, tmp);
             if (int r = tail0->init(dev, C, tmp.data(), tl, st, head_bs, tl)) return r;
         }
-        if (max_len > 2 * T) {                                                  // :387-398
+        if (max_len > 2 * T) {                                                  // :373-384
             const size_t tl = max_len - 2 * T;
             tail.reset(new (std::nothrow) UniformCore());
             if (!tail) return fail(FFTCONV_E_NOMEM, "out of host memory");
@@ -508,15 +508,15 @@ struct TwoStageCore {
         return FFTCONV_OK;
     }
 
-    // fill reached T (:478-505): swap the tail0 buffers, swap the tail buffers,
+    // fill reached T (:464-491): swap the tail0 buffers, swap the tail buffers,
     // and start the tail convolution of this period on the side stream.
     int end_of_period(hipStream_t s) {
-        std::swap(tail_precalculated0, tail_output0);                         // :487-489
-        std::swap(tail_precalculated, tail_output);                           // :497
+        std::swap(tail_precalculated0, tail_output0);                         // :473-475
+        std::swap(tail_precalculated, tail_output);                           // :483
         // work after this point reads the swapped-in tail_precalculated: it is
         // the previous period's tail result, so wait for that kernel here
         if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(s, ev_tail, 0));
-        if (tail) {                                                            // :498-499
+        if (tail) {                                                            // :484-485
             HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
             HIP_TRY(hipStreamWaitEvent(side, ev_main, 0));
             if (int r = tail->process_device(tail_input(), T, tail_output, T, T, side)) return r;
@@ -524,12 +524,12 @@ struct TwoStageCore {
             tail_in_flight = true;
         }
         tin_idx ^= 1;  // the next period fills the other buffer while the tail reads this one
-        tail_input_fill = 0;                                                   // :502-505
+        tail_input_fill = 0;                                                   // :488-491
         precalculated_pos = 0;
         return FFTCONV_OK;
     }
 
-    // TwoStageFFTConvolver::process (:426-509)
+    // TwoStageFFTConvolver::process (:412-495)
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t len, hipStream_t s) {
         if (len > head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
         if (len == 0 || C == 0) return FFTCONV_OK;
@@ -537,14 +537,14 @@ struct TwoStageCore {
             // aligned call: one sub-chunk, and tail0 consumes exactly this block.
             // One launch: head (+ the sub-chunk epilogue) and tail0 as two jobs.
             ProcArgs a{};
-            a.job[0] = head->job(din, is, dout, os, len);                       // :431
-            a.job[0].add0 = tail_precalculated0 + precalculated_pos;            // :453-459
-            a.job[0].add1 = tail_precalculated + precalculated_pos;             // :462-468
+            a.job[0] = head->job(din, is, dout, os, len);                       // :417
+            a.job[0].add0 = tail_precalculated0 + precalculated_pos;            // :439-445
+            a.job[0].add1 = tail_precalculated + precalculated_pos;             // :448-454
             a.job[0].add_stride = (long long)T;
-            a.job[0].tin = tail_input() + tail_input_fill;                     // :473-475
+            a.job[0].tin = tail_input() + tail_input_fill;                     // :459-461
             a.job[0].tin_stride = (long long)T;
             a.njobs = 1;
-            if (tail0) {                                                        // :478-486
+            if (tail0) {                                                        // :464-472
                 a.job[1] = tail0->job(din, is, tail_output0 + tail_input_fill, T, head_bs);
                 a.njobs = 2;
             }
@@ -557,11 +557,11 @@ struct TwoStageCore {
             }
             return FFTCONV_OK;
         }
-        if (int r = head->process_device(din, is, dout, os, len, s)) return r;   // :431
+        if (int r = head->process_device(din, is, dout, os, len, s)) return r;   // :417
         size_t processed = 0;
-        while (processed < len) {                                                 // :441
+        while (processed < len) {                                                 // :427
             const size_t processing = std::min(len - processed, head_bs - (tail_input_fill % head_bs));
-            if (tail_input_fill + processing > T)  // tail_input[fill..fill+processing] out of range (:473-474)
+            if (tail_input_fill + processing > T)  // tail_input[fill..fill+processing] out of range (:459-460)
                 return fail(FFTCONV_E_INVALID, "range end index out of range for slice of length tail_block_size");
             TwoStageAccumArgs a{};
             a.out = dout; a.out_stride = (long long)os;
@@ -569,10 +569,10 @@ struct TwoStageCore {
             a.pos = (int)precalculated_pos; a.in = din; a.in_stride = (long long)is;
             a.sb = (int)processed; a.tail_input = tail_input(); a.fill = (int)tail_input_fill;
             a.cnt = (int)processing;
-            HIP_TRY(launch_twostage_accum(a, (int)C, s));                        // :452-475
+            HIP_TRY(launch_twostage_accum(a, (int)C, s));                        // :438-461
             precalculated_pos += processing;
             tail_input_fill += processing;
-            if (tail_input_fill % head_bs == 0 && tail0) {                        // :478-486
+            if (tail_input_fill % head_bs == 0 && tail0) {                        // :464-472
                 const size_t off = tail_input_fill - head_bs;
                 if (int r = tail0->process_device(tail_input() + off, T, tail_output0 + off, T, head_bs, s)) return r;
             }
@@ -597,7 +597,7 @@ struct TwoStageCore {
         return FFTCONV_OK;
     }
 
-    int reset() {  // :511-525
+    int reset() {  // :497-511
         DeviceGuard g(device);
         HIP_TRY(hipDeviceSynchronize());
         if (int r = head->reset(stream)) return r;
@@ -717,6 +717,15 @@ struct CrossfadeCore {
     // host knows (-1: channels differ), sticky off once they disagree
     long long act[2] = {-1, -1};
     bool pair_ok = false;
+    // A's launch of a fused crossfade step ran but B's failed: A is a block
+    // ahead of B and the crossfader did not advance.  Every later call fails
+    // instead of silently mixing convolvers that are out of step.
+    bool poisoned = false;
+    int check_poisoned() const {
+        return poisoned ? fail(FFTCONV_E_DEVICE, "crossfade handle unusable: an earlier process() failed between "
+                                                  "its two convolvers' launches")
+                        : FFTCONV_OK;
+    }
 
     ~CrossfadeCore() {
         if (stream) {
@@ -779,7 +788,7 @@ struct CrossfadeCore {
     }
 
     // FFTConvolver::update sets active_seg_count = ceil(len / B) on every
-    // channel (:199-204), unless the convolver is empty (:195-197)
+    // channel (:185-190), unless the convolver is empty (:181-183)
     void note_update(int which, size_t len) {
         const UniformCore &u = which ? *b : *a;
         if (u.ir_len == 0) return;
@@ -789,6 +798,7 @@ struct CrossfadeCore {
 
     // Convolution::update (:51-64); host samples, channel c at src + c*stride (stride 0 = shared)
     int update_host(const float *src, size_t len, size_t stride) {
+        if (int r = check_poisoned()) return r;
         DeviceGuard g(device);
         HIP_TRY(hipDeviceSynchronize());
         if (!is_crossfading()) {
@@ -820,6 +830,7 @@ struct CrossfadeCore {
 
     // Convolution::update (:51-64) from device samples, stream-ordered
     int update_device(const float *src, size_t len, size_t stride, hipStream_t s) {
+        if (int r = check_poisoned()) return r;
         if (!is_crossfading()) {
             UniformCore &t = xf.target == 0 ? *b : *a;
             if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
@@ -855,6 +866,7 @@ struct CrossfadeCore {
 
     // Convolution::process (:66-78)
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t out_len, hipStream_t s) {
+        if (int r = check_poisoned()) return r;
         if (out_len > max_buffer_size) return fail(FFTCONV_E_INVALID, "output longer than max_buffer_size (index out of bounds)");
         if (!is_crossfading() && response_pending) {                    // :67-70
             if (int r = swap_device(stored.p, stored_stride, stored_len, s)) return r;
@@ -873,12 +885,18 @@ struct CrossfadeCore {
                 // its own straight into the output -- no mix launch, no buf_b
                 const CrossfadeMixArgs mx = mix_args(dout, os, out_len);
                 if (int r = a->process_device(din, is, buf_a.p, m, m, s, 1, &mx, mix_tab.p)) return r;
-                if (int r = b->process_device(din, is, dout, os, m, s, 2, &mx, mix_tab.p)) return r;
+                if (int r = b->process_device(din, is, dout, os, m, s, 2, &mx, mix_tab.p)) {
+                    poisoned = true;
+                    return r;
+                }
                 xf.advance(out_len);
                 return FFTCONV_OK;
             }
             if (int r = a->process_device(din, is, buf_a.p, m, m, s)) return r;
-            if (int r = b->process_device(din, is, buf_b.p, m, m, s)) return r;
+            if (int r = b->process_device(din, is, buf_b.p, m, m, s)) {
+                poisoned = true;
+                return r;
+            }
             HIP_TRY(launch_crossfade_mix(mix_args(dout, os, out_len), (int)C, s));
             xf.advance(out_len);
             return FFTCONV_OK;
@@ -933,7 +951,7 @@ struct CrossfadeCore {
         device = o.device; C = o.C; max_buffer_size = o.max_buffer_size;
         stored_len = o.stored_len; stored_stride = o.stored_stride;
         xf = o.xf; response_pending = o.response_pending;
-        act[0] = o.act[0]; act[1] = o.act[1]; pair_ok = o.pair_ok;
+        act[0] = o.act[0]; act[1] = o.act[1]; pair_ok = o.pair_ok; poisoned = o.poisoned;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         a.reset(new (std::nothrow) UniformCore());
         b.reset(new (std::nothrow) UniformCore());
@@ -981,7 +999,7 @@ int fftconv_device_count(void) {
 }
 size_t fftconv_complex_size(size_t size) { return size / 2 + 1; }
 
-// compute_tail_block_size, src/fft_convolver.rs:528-540, in f32 exactly as written
+// compute_tail_block_size, src/fft_convolver.rs:514-526, in f32 exactly as written
 size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
     const volatile float FFT_K = 1.5f;
     const volatile float ln2 = logf(2.0f);
@@ -1001,7 +1019,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 255) return fail(FFTCONV_E_INVALID, "variant must be 0..255 (or -1 = auto)");
+    if (variant > 255 || variant < -1) return fail(FFTCONV_E_INVALID, "variant must be 0..255 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }

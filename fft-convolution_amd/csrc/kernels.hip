@@ -57,7 +57,7 @@ template <> struct VecT<2> { using type = float4; };
 template <> struct VecT<1> { using type = float2; };
 
 // Complex multiply-accumulate over one lane-slot, complex_multiply_accumulate
-// (src/fft_convolver.rs:76-88) for 2 bins.  dc/ny carry the products of the
+// (src/fft_convolver.rs:62-74) for 2 bins.  dc/ny carry the products of the
 // packed real bins so that slot 0 can be resolved as (DC, Nyquist).
 struct Acc2 {
     float4 a;
@@ -167,7 +167,7 @@ struct RowStream {
 };
 
 // pre_multiplied = sum_{i=1}^{act-1} H[i] (.) X[(cur+i) % act] over this
-// thread's slots (src/fft_convolver.rs:258-269).  Rows i = 1..act-1 are
+// thread's slots (src/fft_convolver.rs:244-255).  Rows i = 1..act-1 are
 // visited in scan order t = 0..act-2, group g taking t = g (mod G).
 // ZZ: every other block scans the rows backwards (rows read last by one step
 // are read first by the next).  NTL: nontemporal loads.
@@ -312,7 +312,7 @@ __device__ __forceinline__ void dma_16b(void *dst, const void *src, int bytes) {
             __builtin_amdgcn_global_load_lds((gptr_t)(s + base + lane * 16), (lptr_t)(d + base), 16, 0, 0);
 }
 
-// TwoStageFFTConvolver::process sub-chunk (src/fft_convolver.rs:452-475) fused
+// TwoStageFFTConvolver::process sub-chunk (src/fft_convolver.rs:438-461) fused
 // into the head job: output += precalculated0, then += precalculated (two
 // separate adds, like the reference's two loops), and tail_input <- input.
 // Generic form: a pass over the finished output.
@@ -392,7 +392,7 @@ __device__ __forceinline__ void mac_rows_range(AccArr &acc, const float2 *Hc, co
 // Pipelined full-block step (2 <= B <= 512): the common call -- one whole
 // block from an empty input buffer -- when pre[] already holds
 // pre_multiplied for the block at `current` (FLAG_PRE).  The work of
-// FFTConvolver::process (:229-309) is re-timed, not changed:
+// FFTConvolver::process (:215-295) is re-timed, not changed:
 //   wave 0   : R2C of the block -> FDL row `current`; conv = pre + X.H[0];
 //              C2R, x1/N; overlap-add and overlap save -- all out of LDS,
 //              staged by its own LDS-DMA, synchronised at wave level; then
@@ -431,7 +431,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     float2 *prec = J.pre + c * B;
     float *outc = J.out + c * J.out_stride;
     const float *inc = J.in + c * J.in_stride;
-    const int curp = cur > 0 ? cur - 1 : act - 1;  // current after this block (:301-305)
+    const int curp = cur > 0 ? cur - 1 : act - 1;  // current after this block (:287-291)
     const int rsub = F >= 64 ? 0 : lane / F;
     const int f0 = F >= 64 ? lane : lane % F;
 
@@ -451,13 +451,13 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
-        if (J.tin) {  // two-stage: append the block to tail_input (:473-475)
+        if (J.tin) {  // two-stage: append the block to tail_input (:459-461)
             const float *xb = reinterpret_cast<const float *>(bufA);
             float *ti = J.tin + c * J.tin_stride;
             for (int j = lane; j < B; j += 64) ti[j] = xb[j];
         }
         wave_sync();
-        float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :243-255
+        float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
         float2 *Q = Z == bufA ? bufB : bufA;
         float2 *Xcur = Xc + (size_t)cur * B;
         for (int m = lane; m < B; m += 64) {
@@ -466,7 +466,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             Xcur[m] = v;
         }
         wave_sync();
-        bool bad = false;  // conv = pre + X (.) H[0] (:270-275), then the C2R error check
+        bool bad = false;  // conv = pre + X (.) H[0] (:256-261), then the C2R error check
         for (int f = lane; f < F; f += 64) {
             const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
                                        reinterpret_cast<const float4 *>(h0l)[f], f);
@@ -487,17 +487,17 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             for (int m = lane; m < B; m += 64) Q[m] = real_pre<LOG2B, 64>(Z, m, twl);
             wave_sync();
             const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(Q, Z, twl));
-            for (int j = lane; j < B; j += 64) {  // overlap-add (:284-288) + two-stage adds (:453-468)
+            for (int j = lane; j < B; j += 64) {  // overlap-add (:270-274) + two-stage adds (:439-454)
                 float v = y[j] * invN + ovl[j];
                 if (J.add0) {
                     v += p0l[j];
                     if (J.add1) v += p1l[j];
                 }
                 outc[j] = v;
-                ovc[j] = y[B + j] * invN;  // :297-298
+                ovc[j] = y[B + j] * invN;  // :283-284
             }
         } else {
-            // output.fill(0); return (:278-281): the block stays in the input
+            // output.fill(0); return (:264-267): the block stays in the input
             // buffer, fill / current unchanged, pre still describes this block
             float *ibc = J.inbuf + c * B;
             for (int j = lane; j < B; j += 64) {
@@ -544,7 +544,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
 }
 
 // ---------------------------------------------------------------------------
-// Fused UPOLS step: FFTConvolver::process (src/fft_convolver.rs:229-309) for
+// Fused UPOLS step: FFTConvolver::process (src/fft_convolver.rs:215-295) for
 // one channel per workgroup, the whole chunk loop of one call on device.
 //
 // Latency structure: every load that does not depend on the MAC is issued in
@@ -575,7 +575,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
     const float *inc = J.in + c * J.in_stride;
     const int n = J.n;
 
-    if (act == 0) {  // :230-233 -- zero output, state untouched
+    if (act == 0) {  // :216-219 -- zero output, state untouched
         for (int j = tid; j < n; j += NT) outc[j] = 0.f;
         twostage_epilogue<NT>(J, c, outc, inc, n);
         return;
@@ -643,8 +643,8 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
     int processed = 0;
     bool err = false, pre_next = false;
     for (;;) {
-        const bool was_empty = fill == 0;                               // :237
-        const int k = min(n - processed, B - fill);                      // :238-241
+        const bool was_empty = fill == 0;                               // :223
+        const int k = min(n - processed, B - fill);                      // :224-227
         if (processed >= n) {
             // a full-block call that ended on a block boundary: one more MAC
             // pass (no transform) computes the next block's pre_multiplied so
@@ -660,7 +660,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
 #pragma unroll
                 for (int s = 0; s < SPT; ++s) pacc[s] = reinterpret_cast<const vec_t *>(prec)[f0 + s * NT];
             }
-        } else if (was_empty) {                                          // :258-269
+        } else if (was_empty) {                                          // :244-255
             AccT<VEC> acc[SPT];
             mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, J.S, cur, act, flags, f0, g);
             if constexpr (G > 1) {
@@ -683,10 +683,10 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
         }
 
         // forward FFT of the zero-padded input buffer into segments[current]
-        // (:243-255): x[i] = chunk sample, else the carried input buffer.
+        // (:229-241): x[i] = chunk sample, else the carried input buffer.
         if (one_block) {
             // the block is already in bufA (prologue DMA); two-stage: append it
-            // to tail_input from LDS (:473-475)
+            // to tail_input from LDS (:459-461)
             __syncthreads();
             if (J.tin) {
                 const float *xb = reinterpret_cast<const float *>(bufA);
@@ -720,7 +720,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
         }
         __syncthreads();
 
-        // conv = pre_multiplied + segments[current] (.) segments_ir[0] (:270-275)
+        // conv = pre_multiplied + segments[current] (.) segments_ir[0] (:256-261)
         if (owner) {
             const vec_t *q = reinterpret_cast<const vec_t *>(Q);
             vec_t *zc = reinterpret_cast<vec_t *>(Z);
@@ -730,24 +730,24 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
                 const vec_t cv = slot_mac(pacc[s], q[f], reinterpret_cast<const vec_t *>(h0g)[f], f);
                 zc[f] = cv;
                 // realfft's C2R rejects a non-zero DC/Nyquist imaginary part,
-                // which only a non-finite operand can produce (:278-281)
+                // which only a non-finite operand can produce (:264-267)
                 if (f == 0 && !slot0_finite(cv)) s_err = 1;
             }
         }
         __syncthreads();
         if (s_err) { err = true; break; }
 
-        // inverse FFT (:278) with the 1/N of Fft::inverse (:58-60)
+        // inverse FFT (:264) with the 1/N of Fft::inverse (:44-46)
         for (int m = tid; m < B; m += NT) Q[m] = real_pre<LOG2B, NT>(Z, m, tw);
         __syncthreads();
         float2 *Y = lds_cfft<LOG2B, NT, true>(Q, Z, tw);
         const float *y = reinterpret_cast<const float *>(Y);
 
-        // overlap-add (:284-288)
+        // overlap-add (:270-274)
         if (one_block) {
             for (int j = tid; j < B; j += NT) {
                 float v = y[j] * invN + ovl[j];
-                if (J.add0) {  // two-stage sub-chunk adds (:453-468), same rounding order
+                if (J.add0) {  // two-stage sub-chunk adds (:439-454), same rounding order
                     v += p0l[j];
                     if (J.add1) v += p1l[j];
                 }
@@ -756,16 +756,16 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
         } else {
             for (int j = tid; j < k; j += NT) outc[processed + j] = y[fill + j] * invN + ovc[fill + j];
         }
-        const bool complete = fill + k == B;                              // :291-292
+        const bool complete = fill + k == B;                              // :277-278
         if (complete) {
             if (!one_block) __syncthreads();  // every overlap read above is done
-            for (int j = tid; j < B; j += NT) ovc[j] = y[B + j] * invN;  // :297-298
+            for (int j = tid; j < B; j += NT) ovc[j] = y[B + j] * invN;  // :283-284
             if (flags & FLAG_INBUF)
-                for (int j = tid; j < B; j += NT) ibc[j] = 0.f;           // :294
+                for (int j = tid; j < B; j += NT) ibc[j] = 0.f;           // :280
             flags &= ~(FLAG_INBUF | FLAG_PRE);
             flags ^= FLAG_REV;
             fill = 0;
-            cur = cur > 0 ? cur - 1 : act - 1;                            // :301-305
+            cur = cur > 0 ? cur - 1 : act - 1;                            // :287-291
         } else {
             for (int j = tid; j < k; j += NT) ibc[fill + j] = inc[processed + j];
             flags |= FLAG_INBUF;
@@ -944,7 +944,7 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
     // the crossfader's mix_value walk (one lane; hides under the FDL stream)
     if (fuse && a.mix.approaching && tid == 0) mix_walk(a.mix, vtab);
 
-    // both pre_multiplied from one FDL stream (:258-269)
+    // both pre_multiplied from one FDL stream (:244-255)
     vec_t pacc[2][SPT];
     {
         AccT<VEC> accA[SPT], accB[SPT];
@@ -974,7 +974,7 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
     if (tid < 2) s_err[tid] = 0;
     __syncthreads();
 
-    // one R2C (:243-255), written to both FDL rows `current`
+    // one R2C (:229-241), written to both FDL rows `current`
     float2 *Z = lds_cfft<LOG2B, NT, false>(bufA, bufB, twl);
     float2 *W = Z == bufA ? bufB : bufA;
     float2 *XA = Js[0]->X + c * rows + (size_t)cur * B;
@@ -989,7 +989,7 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
 
     for (int j = 0; j < 2; ++j) {
         const ProcJob &J = *Js[j];
-        // conv = pre + X (.) H[0] (:270-275), then the C2R error check
+        // conv = pre + X (.) H[0] (:256-261), then the C2R error check
         if (owner) {
 #pragma unroll
             for (int s = 0; s < SPT; ++s) {
@@ -1008,8 +1008,8 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
             const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, NT, true>(W, Z, twl));
             float *ovc = J.overlap + c * B;
             for (int k = tid; k < B; k += NT) {
-                const float v = y[k] * invN + ovl[j][k];  // :284-288
-                ovc[k] = y[B + k] * invN;                  // :297-298
+                const float v = y[k] * invN + ovl[j][k];  // :270-274
+                ovc[k] = y[B + k] * invN;                  // :283-284
                 if (!fuse) {
                     outc[k] = v;
                 } else if (j == 0) {
@@ -1020,7 +1020,7 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
             }
             if (tid == 0) J.state[c] = make_int4(cur > 0 ? cur - 1 : act - 1, act, 0, la_clear((flags & ~FLAG_INBUF) ^ FLAG_REV, a));
         } else {
-            // output.fill(0); return (:278-281): block kept in the input buffer
+            // output.fill(0); return (:264-267): block kept in the input buffer
             float *ibc = J.inbuf + c * B;
             for (int k = tid; k < B; k += NT) {
                 if (!fuse) outc[k] = 0.f;
@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(NT, 2) void upols_pair_kernel(ProcArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// IR partition: FFTConvolver::init (:145-156) / update (:204-226).
+// IR partition: FFTConvolver::init (:131-142) / update (:190-212).
 // grid (S, channels): workgroup (i, c) transforms segment i of channel
 // chan0 + c; segments at or past ceil(len_active / B) are zeroed.
 // ---------------------------------------------------------------------------
@@ -1095,7 +1095,7 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
     const long long active = (a.len_active + B - 1) / B;
 
     if (a.update_state && i == 0) {
-        // update(): zero overlap / pre_multiplied / conv, set active (:199-204)
+        // update(): zero overlap / pre_multiplied / conv, set active (:185-190)
         for (int j = tid; j < B; j += NT) {
             a.overlap[c * B + j] = 0.f;
             a.pre[c * B + j] = make_float2(0.f, 0.f);
@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
             a.state[c].w &= ~(FLAG_PRE | LA_MASK | SEQ_MASK);  // the stored pre / window used the old response
         }
     }
-    if (i >= active) {  // :224-226
+    if (i >= active) {  // :210-212
         for (int j = tid; j < B; j += NT) row[j] = make_float2(0.f, 0.f);
         return;
     }
@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
     const long long active = (a.len_active + B - 1) / B;
     dma_16b<256>(twl, a.tw, 2 * B * (int)sizeof(float2));
     if (a.update_state && blockIdx.x == 0) {
-        // update(): zero overlap / pre_multiplied / conv, set active (:199-204)
+        // update(): zero overlap / pre_multiplied / conv, set active (:185-190)
         for (int j = tid; j < B; j += 256) {
             a.overlap[c * B + j] = 0.f;
             a.pre[c * B + j] = make_float2(0.f, 0.f);
@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
         const int i = (blockIdx.x * 4 + wave) * IR_SPW + q;
         if (i >= a.S) break;
         float2 *row = a.H + c * rows + (size_t)i * B;
-        if (i >= active) {  // :224-226
+        if (i >= active) {  // :210-212
             for (int m = lane; m < B; m += 64) row[m] = make_float2(0.f, 0.f);
             continue;
         }
@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// TwoStage sub-chunk (src/fft_convolver.rs:452-475): output += precalculated0
+// TwoStage sub-chunk (src/fft_convolver.rs:438-461): output += precalculated0
 // then += precalculated (two passes, like the reference), and append the
 // input to tail_input.
 // ---------------------------------------------------------------------------
@@ -1200,7 +1200,7 @@ __global__ void twostage_accum_kernel(TwoStageAccumArgs a) {
     }
 }
 
-// FFTConvolver::reset (src/fft_convolver.rs:310-320) scalar part: current = 0,
+// FFTConvolver::reset (src/fft_convolver.rs:296-306) scalar part: current = 0,
 // input_buffer_fill = 0; active_seg_count is kept.
 __global__ void reset_state_kernel(int4 *state, int channels) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;

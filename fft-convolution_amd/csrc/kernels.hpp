@@ -43,7 +43,7 @@ int get_pipeline_lag();
 
 // One convolver batch's call (FFTConvolver::process over `n` samples of every
 // channel), optionally with the two-stage epilogue of the head block
-// (src/fft_convolver.rs:452-475): out[j] += add0[j], then += add1[j], and
+// (src/fft_convolver.rs:438-461): out[j] += add0[j], then += add1[j], and
 // tin[j] = in[j], applied after the call.
 struct ProcJob {
     const float2 *H;       // [C][S][B] packed IR spectra

@@ -3,7 +3,7 @@
 // after its helpers).
 //
 // The reference computes, for every block s of a channel (src/fft_convolver.rs
-// :258-275),
+// :244-261),
 //     conv_s = sum_{i=1}^{act-1} H[i] (.) X_{s-i}  +  H[0] (.) X_s
 // where X_b is the spectrum of block b (FDL row (current + age) % act).  Every
 // step re-reads all act rows of H and of the FDL: 16 B per bin-row, 773 KB
@@ -35,7 +35,7 @@
 // act) in NG fixed groups (even groups descending, odd ascending, so that
 // neighbouring groups read their shared window rows at the same time) combined
 // sequentially within a far part and then over the parts.  Then
-//     pre = near + (mid + far),   conv = pre + H[0] (.) X_s   (slot_mac, :270-275).
+//     pre = near + (mid + far),   conv = pre + H[0] (.) X_s   (slot_mac, :256-261).
 // An anchor's accumulator for step a+j visits exactly the rows and blocks the
 // step a+j would, in the same order, so a step served from windows and a step
 // that sums everything itself (entry, after update / reset / partial calls,
@@ -73,7 +73,7 @@ __device__ __forceinline__ LaH la_ops(float4 h, bool z0) {
     o.q1 = f2v{-h.w, h.w};
     return o;
 }
-// complex_multiply_accumulate (src/fft_convolver.rs:76-88) over 2 bins:
+// complex_multiply_accumulate (src/fft_convolver.rs:62-74) over 2 bins:
 // re = fma(-h.im, x.im, fma(h.re, x.re, re)), im = fma(h.im, x.re, fma(h.re, x.im, im))
 struct LaAcc {
     f2v a01, a23;
@@ -236,7 +236,21 @@ struct LaGeo {
 };
 
 // the anchor's view of channel c: its ring position, window and length, or
-// false if this launch opens no window of the level (period P) at c
+// false if this launch opens no window of the level (period P) at c.
+//
+// Memory-model assumption (the one shared word of a launch).  The channel's
+// step workgroup stores state[c] once, as ONE 16-byte store from one lane
+// (global_store_dwordx4 of an aligned int4), and an anchor reads it as ONE
+// 16-byte load.  Both are single requests to one 64-byte line: the L2 that
+// holds the line applies the store whole, and a line is written back / filled
+// whole, so a reader on any XCD observes either the pre-step word or the
+// post-step word, never a mix of the two.  (Typically the pre-step one: the
+// writer's L2 keeps the dirty line until the launch's end-of-kernel release,
+// and the reader's L2 was invalidated at launch start.)  Either observation
+// is handled exactly: the launch tag (SEQ_MASK) in the word says which one
+// it is, and both branches below rebuild the same ring position and window.
+// Nothing else of the step is read by an anchor (FDL ages >= 1 only, the
+// other window of each level).
 template <int LOG2B>
 __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int c, int P, int &cur, int &act, int &win,
                                                 int &d) {
@@ -359,7 +373,7 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
 
 // ---------------------------------------------------------------------------
 // Step workgroup: one full block of each of NCH channels (FFTConvolver::
-// process :229-309 for the common call).  Wave k < NCH runs channel k's
+// process :215-295 for the common call).  Wave k < NCH runs channel k's
 // transform chain (R2C of the block into FDL row `current`, then conv, C2R,
 // overlap-add) while the other waves form every channel's
 // pre = near + (mid + far), the mid / far partials from their windows or --
@@ -509,13 +523,13 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         } else {
             wave_sync();
         }
-        if (J.tin) {  // two-stage: append the block to tail_input (:473-475)
+        if (J.tin) {  // two-stage: append the block to tail_input (:459-461)
             const float *xb = reinterpret_cast<const float *>(bufA);
             float *ti = J.tin + c * J.tin_stride;
             for (int j = lane; j < B; j += 64) ti[j] = xb[j];
         }
         wave_sync();
-        Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :243-255
+        Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
         Q = Z == bufA ? bufB : bufA;
         float2 *Xcur = J.X + c * rows + (size_t)cur * B;
         for (int m = lane; m < B; m += 64) {
@@ -610,7 +624,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     float *outc = J.out + c * J.out_stride;
     float *ovc = J.overlap + c * B;
     // crossfade, B's launch: out = mix(A's block, this block) (:75-77)
-    bool bad = false;  // conv = pre + X (.) H[0] (:270-275), then the C2R error check
+    bool bad = false;  // conv = pre + X (.) H[0] (:256-261), then the C2R error check
     for (int f = lane; f < F; f += 64) {
         const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
                                    reinterpret_cast<const float4 *>(h0l)[f], f);
@@ -625,7 +639,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         for (int m = lane; m < B; m += 64) Q[m] = real_pre<LOG2B, 64>(Z, m, twl);
         wave_sync();
         const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(Q, Z, twl));
-        for (int j = lane; j < B; j += 64) {  // overlap-add (:284-288) + two-stage adds (:453-468)
+        for (int j = lane; j < B; j += 64) {  // overlap-add (:270-274) + two-stage adds (:439-454)
             float v = y[j] * invN + ovl[j];
             if (J.add0) {
                 v += p0l[j];
@@ -633,10 +647,10 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             }
             if constexpr (XF == 2) v = mix_select(p0l[j], v, p1l[j]);
             outc[j] = v;
-            ovc[j] = y[B + j] * invN;  // :297-298
+            ovc[j] = y[B + j] * invN;  // :283-284
         }
         if (lane == 0) {
-            const int curp = cur > 0 ? cur - 1 : act - 1;  // :301-305
+            const int curp = cur > 0 ? cur - 1 : act - 1;  // :287-291
             int nf = (keep ^ FLAG_REV) | tag;
             // far window: open (a far anchor this launch), advance, or drop
             if (la_sched((int)c, a, LA_DF))
@@ -651,7 +665,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             J.state[c] = make_int4(curp, act, 0, nf);
         }
     } else {
-        // output.fill(0); return (:278-281): the block stays in the input
+        // output.fill(0); return (:264-267): the block stays in the input
         // buffer, fill / current unchanged; the windows are dropped
         const float *inc = J.in + c * J.in_stride;
         float *ibc = J.inbuf + c * B;

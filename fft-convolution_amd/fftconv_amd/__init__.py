@@ -1,9 +1,9 @@
 """fftconv_amd -- Python mirror of the reference's `Convolution` trait over the
 MI355X C ABI (include/fftconv.h, libfftconv_amd.so).
 
-    FFTConvolver.init(response, max_block_size, max_response_length)   src/fft_convolver.rs:119
+    FFTConvolver.init(response, max_block_size, max_response_length)   src/fft_convolver.rs:105
     .update(response) / .reset() / .process(input[, out_len]) / .clone()
-    TwoStageFFTConvolver.init(...)                                      src/fft_convolver.rs:354
+    TwoStageFFTConvolver.init(...)                                      src/fft_convolver.rs:340
     CrossfadeConvolver.init(...) / CrossfadeConvolver.new(conv, ...)    src/crossfade_convolver.rs:19-49
 
 Every object is a batch of `channels` independent convolvers on one GPU
@@ -247,7 +247,7 @@ class _Base:
 
 
 class FFTConvolver(_Base):
-    """FFTConvolver, src/fft_convolver.rs:100-321 (a batch of `channels`)."""
+    """FFTConvolver, src/fft_convolver.rs:86-307 (a batch of `channels`)."""
 
     _prefix = "uniform"
 
@@ -307,7 +307,7 @@ class FFTConvolver(_Base):
 
 
 class TwoStageFFTConvolver(_Base):
-    """TwoStageFFTConvolver, src/fft_convolver.rs:337-526."""
+    """TwoStageFFTConvolver, src/fft_convolver.rs:323-526."""
 
     _prefix = "twostage"
 

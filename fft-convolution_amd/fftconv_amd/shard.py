@@ -1,7 +1,7 @@
 """Channel sharding across GPUs (one process per GPU).
 
 Channels are fully independent convolvers (the reference is one instance per
-channel, src/fft_convolver.rs:100-116), so a node-level batch of C channels is
+channel, src/fft_convolver.rs:86-102), so a node-level batch of C channels is
 split into contiguous per-rank blocks with no data-path exchange.  Synthetic
 IRs and dry blocks are seeded by *global* channel id, so a channel's output is
 bit-identical whatever the world size.  The only collective is the optional

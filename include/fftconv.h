@@ -23,7 +23,7 @@
  * message is available from fftconv_last_error().  A runtime FFT error
  * (realfft's C2R rejecting a non-finite DC/Nyquist bin) zero-fills that
  * channel's output and leaves its block state where the reference leaves it
- * (src/fft_convolver.rs:278-281); it is not an error status.
+ * (src/fft_convolver.rs:264-267); it is not an error status.
  *
  * There is no CPU fallback: creating a handle without a usable gfx950 device
  * fails with FFTCONV_E_DEVICE.
@@ -48,16 +48,16 @@ enum {
     FFTCONV_E_NOMEM = -5
 };
 
-typedef struct fftconv_uniform fftconv_uniform;     /* FFTConvolver        src/fft_convolver.rs:100-321 */
-typedef struct fftconv_twostage fftconv_twostage;   /* TwoStageFFTConvolver src/fft_convolver.rs:337-526 */
+typedef struct fftconv_uniform fftconv_uniform;     /* FFTConvolver        src/fft_convolver.rs:86-307 */
+typedef struct fftconv_twostage fftconv_twostage;   /* TwoStageFFTConvolver src/fft_convolver.rs:323-512 */
 typedef struct fftconv_crossfade fftconv_crossfade; /* CrossfadeConvolver<FFTConvolver> src/crossfade_convolver.rs:10-105 */
 
 /* ---- library ----------------------------------------------------------- */
 int fftconv_abi_version(void);
 const char *fftconv_last_error(void);            /* thread-local, "" if none */
 int fftconv_device_count(void);                   /* visible HIP devices, 0 if none */
-size_t fftconv_complex_size(size_t size);         /* src/fft_convolver.rs:66-68 */
-size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /* :534-540 */
+size_t fftconv_complex_size(size_t size);         /* src/fft_convolver.rs:52-54 */
+size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /* :520-526 */
 /* Tuning knob (process-wide): spectral-MAC scan variant of the fused kernel,
  * -1 = automatic (default: nontemporal loads when the per-step H+X stream
  * exceeds the Infinity Cache, plain loads otherwise -- the load policy never
@@ -78,10 +78,14 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
  * transforms (init / update) one segment per workgroup (by default one per
  * wave for 64 <= B <= 1024; bit-identical).
  * Lookahead (automatic for standalone FFTConvolver batches with
- * 128 <= B <= 512 and >= 27 segments): the far FDL rows' terms of the next
- * 8 full blocks are summed ahead in one pass over H and the FDL, so a
- * full-block call streams ~1/8 of the rows; its summation order does not
- * depend on the channel index, the shard or the call history.
+ * 128 <= B <= 512 and >= 40 segments, full-block calls from an empty input
+ * buffer): the FDL sum of each block is re-associated in time over three
+ * levels -- the step sums rows 1..5 itself, a mid anchor every 5 blocks sums
+ * rows 6..32 for the next 5 blocks, a far anchor every 32 blocks sums rows
+ * >= 33 for the next 32 blocks -- so a full-block call streams ~1/9 of the
+ * reference's bytes; its summation order does not depend on the channel
+ * index, the shard or the call history (bit-identical to summing every row).
+ * -1 selects automatic; any other negative value is FFTCONV_E_INVALID.
  * Results agree within f32 rounding across variants. */
 int fftconv_set_kernel_variant(int variant);
 int fftconv_get_kernel_variant(void);
@@ -93,7 +97,7 @@ int fftconv_set_pipeline_lag(int rows);
 int fftconv_get_pipeline_lag(void);
 
 /* ---- FFTConvolver (uniformly partitioned, zero latency) ---------------- */
-/* FFTConvolver::init, src/fft_convolver.rs:119-186.  NULL on error. */
+/* FFTConvolver::init, src/fft_convolver.rs:105-186.  NULL on error. */
 fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len,
                                       size_t max_block_size, size_t max_response_length);
 /* Batched init on `device`: channel c's response is responses[c*response_stride ..
@@ -101,7 +105,7 @@ fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len
 fftconv_uniform *fftconv_uniform_init_batch(int device, size_t channels, const float *responses,
                                             size_t response_len, size_t response_stride,
                                             size_t max_block_size, size_t max_response_length);
-/* FFTConvolver::update, src/fft_convolver.rs:188-227; every channel gets the
+/* FFTConvolver::update, src/fft_convolver.rs:174-213; every channel gets the
  * same response.  No allocation (staging is reserved at init). */
 int fftconv_uniform_update(fftconv_uniform *h, const float *response, size_t response_len);
 /* Per-channel responses, host memory, channel c at responses[c*stride ..]. */
@@ -115,9 +119,9 @@ int fftconv_uniform_update_channel(fftconv_uniform *h, size_t channel, const flo
  * (NULL = own stream) without a host synchronisation or an allocation. */
 int fftconv_uniform_update_device(fftconv_uniform *h, const float *d_responses, size_t response_len,
                                   size_t response_stride, void *hip_stream);
-/* FFTConvolver::reset, src/fft_convolver.rs:310-320 (all channels). */
+/* FFTConvolver::reset, src/fft_convolver.rs:296-306 (all channels). */
 int fftconv_uniform_reset(fftconv_uniform *h);
-/* FFTConvolver::process, src/fft_convolver.rs:229-309, host buffers:
+/* FFTConvolver::process, src/fft_convolver.rs:215-295, host buffers:
  * input [channels][input_len], output [channels][output_len]; reads
  * input[0..output_len] of each channel (input_len >= output_len, else
  * FFTCONV_E_INVALID like the reference's slice panic).  Synchronous. */
@@ -153,10 +157,10 @@ fftconv_twostage *fftconv_twostage_init(const float *response, size_t response_l
 fftconv_twostage *fftconv_twostage_init_batch(int device, size_t channels, const float *responses,
                                               size_t response_len, size_t response_stride,
                                               size_t max_block_size, size_t max_response_length);
-/* todo!() in the reference (src/fft_convolver.rs:422-424): FFTCONV_E_UNIMPLEMENTED. */
+/* todo!() in the reference (src/fft_convolver.rs:408-410): FFTCONV_E_UNIMPLEMENTED. */
 int fftconv_twostage_update(fftconv_twostage *h, const float *response, size_t response_len);
 int fftconv_twostage_reset(fftconv_twostage *h);
-/* len must be <= max_block_size (assert at src/fft_convolver.rs:428); input and
+/* len must be <= max_block_size (assert at src/fft_convolver.rs:414); input and
  * output both [channels][len]. */
 int fftconv_twostage_process(fftconv_twostage *h, const float *input, float *output, size_t len);
 int fftconv_twostage_process_device(fftconv_twostage *h, const float *d_input, size_t in_stride,

@@ -8,10 +8,10 @@
  *
  * It restates, line by line, the state machines of Sin-tel/fft-convolution
  * (paths relative to the reference checkout):
- *   src/fft_convolver.rs:15-98    Fft wrapper + primitives (complex_size,
+ *   src/fft_convolver.rs:1-84    Fft wrapper + primitives (complex_size,
  *                                 copy_and_pad, complex_multiply_accumulate, sum)
- *   src/fft_convolver.rs:100-321  FFTConvolver (init/update/process/reset)
- *   src/fft_convolver.rs:337-540  TwoStageFFTConvolver + compute_tail_block_size
+ *   src/fft_convolver.rs:86-307  FFTConvolver (init/update/process/reset)
+ *   src/fft_convolver.rs:323-526  TwoStageFFTConvolver + compute_tail_block_size
  *   src/crossfade_convolver.rs    CrossfadeConvolver, Crossfader, RaisedCosineMixer
  *
  * The reference's FFT arithmetic lives in the third-party crates realfft ^3.3
@@ -22,7 +22,7 @@
  * computed in f64 and rounded to f32 (rustfft's compute_twiddle).  The C2R
  * rejects a non-zero imaginary part in the DC/Nyquist bin with an error after
  * computing (realfft ComplexToRealEven::process); the reference then zero-fills
- * its output (src/fft_convolver.rs:278-281).  Bit-level parity with rustfft is
+ * its output (src/fft_convolver.rs:264-267).  Bit-level parity with rustfft is
  * unpinned (crate absent); the oracle is pinned by the reference's own
  * known-answer / self-consistency tests (src/tests.rs, inline #[test]s) and by
  * an independent f64 direct convolution (see tests/test_oracle.py).
@@ -62,7 +62,7 @@ static void rfft_free(rfft_t *f) {
     memset(f, 0, sizeof(*f));
 }
 
-/* Fft::init (src/fft_convolver.rs:44-48); N is always even here (2*B). */
+/* Fft::init (src/fft_convolver.rs:30-34); N is always even here (2*B). */
 static int rfft_init(rfft_t *f, size_t n) {
     memset(f, 0, sizeof(*f));
     f->n = n;
@@ -120,7 +120,7 @@ static void cfft(const rfft_t *f, cpx *z, int inverse) {
     }
 }
 
-/* Fft::forward (src/fft_convolver.rs:50-53): unnormalised R2C, N -> N/2+1. */
+/* Fft::forward (src/fft_convolver.rs:36-39): unnormalised R2C, N -> N/2+1. */
 static void rfft_forward(const rfft_t *f, const float *x, cpx *out) {
     size_t m = f->m;
     if (f->n == 0) return;
@@ -139,7 +139,7 @@ static void rfft_forward(const rfft_t *f, const float *x, cpx *out) {
     }
 }
 
-/* Fft::inverse minus the 1/N (src/fft_convolver.rs:55-63): unnormalised C2R.
+/* Fft::inverse minus the 1/N (src/fft_convolver.rs:41-49): unnormalised C2R.
  * Returns 1 (FftError::InputValues) when DC or Nyquist carries a non-zero
  * imaginary part; the output is still computed, as realfft does. */
 static int rfft_inverse(const rfft_t *f, cpx *in, float *x) {
@@ -164,7 +164,7 @@ static int rfft_inverse(const rfft_t *f, cpx *in, float *x) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* primitives: src/fft_convolver.rs:66-98                                    */
+/* primitives: src/fft_convolver.rs:52-84                                    */
 /* ------------------------------------------------------------------------ */
 size_t oracle_complex_size(size_t size) { return size / 2 + 1; }
 
@@ -188,7 +188,7 @@ static void vsum(float *r, const float *a, const float *b, size_t len) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* FFTConvolver: src/fft_convolver.rs:100-321                                */
+/* FFTConvolver: src/fft_convolver.rs:86-307                                */
 /* ------------------------------------------------------------------------ */
 typedef struct {
     size_t ir_len, block_size, seg_count, active_seg_count;
@@ -216,22 +216,22 @@ void ou_free(ou_t *c) {
 /* Default::default() -- every field zero / empty, length-0 FFT plans. */
 ou_t *ou_default(void) { return (ou_t *)calloc(1, sizeof(ou_t)); }
 
-/* FFTConvolver::init (src/fft_convolver.rs:119-186).  NULL = panic. */
+/* FFTConvolver::init (src/fft_convolver.rs:105-172).  NULL = panic. */
 ou_t *ou_init(const float *ir, size_t ir_len_in, size_t block_size_in, size_t max_len) {
-    if (max_len < ir_len_in) return NULL; /* :120-124 */
+    if (max_len < ir_len_in) return NULL; /* :106-110 */
     ou_t *c = (ou_t *)calloc(1, sizeof(ou_t));
     if (!c) return NULL;
-    float *padded = (float *)calloc(max_len ? max_len : 1, sizeof(float)); /* :125-126 */
+    float *padded = (float *)calloc(max_len ? max_len : 1, sizeof(float)); /* :111-112 */
     if (ir_len_in) memcpy(padded, ir, ir_len_in * sizeof(float));
     size_t ir_len = max_len;
-    size_t B = next_pow2(block_size_in);                            /* :129 */
-    size_t N = 2 * B;                                               /* :130 */
-    size_t S = (size_t)ceil((double)ir_len / (double)B);            /* :131 */
-    size_t K = oracle_complex_size(N);                              /* :133 */
+    size_t B = next_pow2(block_size_in);                            /* :115 */
+    size_t N = 2 * B;                                               /* :116 */
+    size_t S = (size_t)ceil((double)ir_len / (double)B);            /* :117 */
+    size_t K = oracle_complex_size(N);                              /* :119 */
     c->ir_len = ir_len; c->block_size = B; c->seg_count = S; c->active_seg_count = S;
-    if (rfft_init(&c->fft, N)) goto fail;                           /* :136-137 */
+    if (rfft_init(&c->fft, N)) goto fail;                           /* :122-123 */
     c->fft_buffer = (float *)calloc(N, sizeof(float));
-    c->segments = (cpx *)calloc(S * K + 1, sizeof(cpx));             /* :141 */
+    c->segments = (cpx *)calloc(S * K + 1, sizeof(cpx));             /* :127 */
     c->segments_ir = (cpx *)calloc(S * K + 1, sizeof(cpx));
     c->pre_multiplied = (cpx *)calloc(K, sizeof(cpx));
     c->conv = (cpx *)calloc(K, sizeof(cpx));
@@ -239,7 +239,7 @@ ou_t *ou_init(const float *ir, size_t ir_len_in, size_t block_size_in, size_t ma
     c->input_buffer = (float *)calloc(B, sizeof(float));
     if (!c->fft_buffer || !c->segments || !c->segments_ir || !c->pre_multiplied || !c->conv ||
         !c->overlap || !c->input_buffer) goto fail;
-    for (size_t i = 0; i < S; i++) {                                /* :145-156 */
+    for (size_t i = 0; i < S; i++) {                                /* :131-142 */
         size_t remaining = ir_len - i * B;
         size_t size_copy = remaining >= B ? B : remaining;
         copy_and_pad(c->fft_buffer, N, padded + i * B, size_copy);
@@ -253,45 +253,45 @@ fail:
     return NULL;
 }
 
-/* FFTConvolver::update (src/fft_convolver.rs:188-227).  -1 = panic. */
+/* FFTConvolver::update (src/fft_convolver.rs:174-213).  -1 = panic. */
 int ou_update(ou_t *c, const float *response, size_t new_ir_len) {
-    if (new_ir_len > c->ir_len) return -1;                          /* :191-193 */
-    if (c->ir_len == 0) return 0;                                   /* :195-197 */
+    if (new_ir_len > c->ir_len) return -1;                          /* :177-179 */
+    if (c->ir_len == 0) return 0;                                   /* :181-183 */
     size_t B = c->block_size, N = 2 * B, K = ou_K(c);
-    memset(c->fft_buffer, 0, N * sizeof(float));                    /* :199-202 */
+    memset(c->fft_buffer, 0, N * sizeof(float));                    /* :185-188 */
     memset(c->conv, 0, K * sizeof(cpx));
     memset(c->pre_multiplied, 0, K * sizeof(cpx));
     memset(c->overlap, 0, B * sizeof(float));
-    c->active_seg_count = (size_t)ceil((double)new_ir_len / (double)B); /* :204 */
-    for (size_t i = 0; i < c->active_seg_count; i++) {              /* :207-221 */
+    c->active_seg_count = (size_t)ceil((double)new_ir_len / (double)B); /* :190 */
+    for (size_t i = 0; i < c->active_seg_count; i++) {              /* :193-207 */
         size_t remaining = new_ir_len - i * B;
         size_t size_copy = remaining >= B ? B : remaining;
         copy_and_pad(c->fft_buffer, N, response + i * B, size_copy);
         rfft_forward(&c->fft, c->fft_buffer, c->segments_ir + i * K);
     }
-    for (size_t i = c->active_seg_count; i < c->seg_count; i++)     /* :224-226 */
+    for (size_t i = c->active_seg_count; i < c->seg_count; i++)     /* :210-212 */
         memset(c->segments_ir + i * K, 0, K * sizeof(cpx));
     return 0;
 }
 
-/* FFTConvolver::process (src/fft_convolver.rs:229-309).  Reads
+/* FFTConvolver::process (src/fft_convolver.rs:215-295).  Reads
  * input[0..out_len]; the caller guarantees input holds that many samples. */
 void ou_process(ou_t *c, const float *input, float *output, size_t out_len) {
-    if (c->active_seg_count == 0) {                                 /* :230-233 */
+    if (c->active_seg_count == 0) {                                 /* :216-219 */
         memset(output, 0, out_len * sizeof(float));
         return;
     }
     size_t B = c->block_size, N = 2 * B, K = ou_K(c);
     size_t processed = 0;
-    while (processed < out_len) {                                   /* :236 */
-        int was_empty = c->input_buffer_fill == 0;                  /* :237 */
-        size_t processing = out_len - processed;                    /* :238-241 */
+    while (processed < out_len) {                                   /* :222 */
+        int was_empty = c->input_buffer_fill == 0;                  /* :223 */
+        size_t processing = out_len - processed;                    /* :224-227 */
         if (B - c->input_buffer_fill < processing) processing = B - c->input_buffer_fill;
-        size_t pos = c->input_buffer_fill;                          /* :243-245 */
+        size_t pos = c->input_buffer_fill;                          /* :229-231 */
         memcpy(c->input_buffer + pos, input + processed, processing * sizeof(float));
-        copy_and_pad(c->fft_buffer, N, c->input_buffer, B);         /* :248 */
-        rfft_forward(&c->fft, c->fft_buffer, c->segments + c->current * K); /* :249-255 */
-        if (was_empty) {                                            /* :258-269 */
+        copy_and_pad(c->fft_buffer, N, c->input_buffer, B);         /* :234 */
+        rfft_forward(&c->fft, c->fft_buffer, c->segments + c->current * K); /* :235-241 */
+        if (was_empty) {                                            /* :244-255 */
             memset(c->pre_multiplied, 0, K * sizeof(cpx));
             for (size_t i = 1; i < c->active_seg_count; i++) {
                 size_t index_ir = i;
@@ -300,16 +300,16 @@ void ou_process(ou_t *c, const float *input, float *output, size_t out_len) {
                                             c->segments + index_audio * K, K);
             }
         }
-        memcpy(c->conv, c->pre_multiplied, K * sizeof(cpx));        /* :270 */
-        complex_multiply_accumulate(c->conv, c->segments + c->current * K, c->segments_ir, K); /* :271-275 */
-        if (rfft_inverse(&c->fft, c->conv, c->fft_buffer)) {        /* :278-281 */
+        memcpy(c->conv, c->pre_multiplied, K * sizeof(cpx));        /* :256 */
+        complex_multiply_accumulate(c->conv, c->segments + c->current * K, c->segments_ir, K); /* :257-261 */
+        if (rfft_inverse(&c->fft, c->conv, c->fft_buffer)) {        /* :264-267 */
             memset(output, 0, out_len * sizeof(float));
             return;
         }
-        for (size_t i = 0; i < N; i++) c->fft_buffer[i] /= (float)N; /* Fft::inverse :58-60 */
-        vsum(output + processed, c->fft_buffer + pos, c->overlap + pos, processing); /* :284-288 */
-        c->input_buffer_fill += processing;                         /* :291 */
-        if (c->input_buffer_fill == B) {                            /* :292-306 */
+        for (size_t i = 0; i < N; i++) c->fft_buffer[i] /= (float)N; /* Fft::inverse :44-46 */
+        vsum(output + processed, c->fft_buffer + pos, c->overlap + pos, processing); /* :270-274 */
+        c->input_buffer_fill += processing;                         /* :277 */
+        if (c->input_buffer_fill == B) {                            /* :278-292 */
             memset(c->input_buffer, 0, B * sizeof(float));
             c->input_buffer_fill = 0;
             memcpy(c->overlap, c->fft_buffer + B, B * sizeof(float));
@@ -319,7 +319,7 @@ void ou_process(ou_t *c, const float *input, float *output, size_t out_len) {
     }
 }
 
-/* FFTConvolver::reset (src/fft_convolver.rs:310-320). */
+/* FFTConvolver::reset (src/fft_convolver.rs:296-306). */
 void ou_reset(ou_t *c) {
     size_t B = c->block_size, K = ou_K(c);
     if (c->overlap) memset(c->overlap, 0, B * sizeof(float));
@@ -372,7 +372,7 @@ size_t ou_current(const ou_t *c) { return c->current; }
 size_t ou_fill(const ou_t *c) { return c->input_buffer_fill; }
 
 /* ------------------------------------------------------------------------ */
-/* compute_tail_block_size: src/fft_convolver.rs:528-540 (f32 arithmetic)    */
+/* compute_tail_block_size: src/fft_convolver.rs:514-526 (f32 arithmetic)    */
 /* ------------------------------------------------------------------------ */
 size_t oracle_compute_tail_block_size(size_t head_len, size_t response_len) {
     const float FFT_K = 1.5f;
@@ -388,7 +388,7 @@ size_t oracle_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* TwoStageFFTConvolver: src/fft_convolver.rs:337-526                        */
+/* TwoStageFFTConvolver: src/fft_convolver.rs:323-512                        */
 /* ------------------------------------------------------------------------ */
 typedef struct {
     size_t head_block_size, tail_block_size;
@@ -405,32 +405,32 @@ void ots_free(ots_t *t) {
     free(t);
 }
 
-/* TwoStageFFTConvolver::init (:354-420).  NULL = panic. */
+/* TwoStageFFTConvolver::init (:340-406).  NULL = panic. */
 ots_t *ots_init(const float *ir, size_t ir_len_in, size_t block_size, size_t max_len) {
-    size_t head_bs = block_size;                                     /* :355 */
-    size_t T = oracle_compute_tail_block_size(block_size, max_len);  /* :356 */
-    if (max_len < ir_len_in) return NULL;                            /* :358-362 */
+    size_t head_bs = block_size;                                     /* :341 */
+    size_t T = oracle_compute_tail_block_size(block_size, max_len);  /* :342 */
+    if (max_len < ir_len_in) return NULL;                            /* :344-348 */
     ots_t *t = (ots_t *)calloc(1, sizeof(ots_t));
     if (!t) return NULL;
-    float *padded = (float *)calloc(max_len ? max_len : 1, sizeof(float)); /* :363-364 */
+    float *padded = (float *)calloc(max_len ? max_len : 1, sizeof(float)); /* :349-350 */
     if (ir_len_in) memcpy(padded, ir, ir_len_in * sizeof(float));
     t->head_block_size = head_bs;
     t->tail_block_size = T;
-    size_t head_ir_len = max_len < T ? max_len : T;                  /* :366-368 */
+    size_t head_ir_len = max_len < T ? max_len : T;                  /* :352-354 */
     t->head = ou_init(padded, head_ir_len, head_bs, head_ir_len);
-    if (max_len > T) {                                               /* :370-382 */
+    if (max_len > T) {                                               /* :356-368 */
         size_t tl = max_len - T < T ? max_len - T : T;
         t->tail0 = ou_init(padded + T, tl, head_bs, tl);
     } else {
         t->tail0 = ou_default();
     }
-    if (max_len > 2 * T) {                                           /* :387-398 */
+    if (max_len > 2 * T) {                                           /* :373-384 */
         size_t tl = max_len - 2 * T;
         t->tail = ou_init(padded + 2 * T, tl, T, tl);
     } else {
         t->tail = ou_default();
     }
-    t->tail_output0 = (float *)calloc(T, sizeof(float));             /* :384-402 */
+    t->tail_output0 = (float *)calloc(T, sizeof(float));             /* :370-388 */
     t->tail_precalculated0 = (float *)calloc(T, sizeof(float));
     t->tail_output = (float *)calloc(T, sizeof(float));
     t->tail_precalculated = (float *)calloc(T, sizeof(float));
@@ -444,32 +444,32 @@ ots_t *ots_init(const float *ir, size_t ir_len_in, size_t block_size, size_t max
     return t;
 }
 
-/* TwoStageFFTConvolver::process (:426-509).  -1 = the assert at :428. */
+/* TwoStageFFTConvolver::process (:412-495).  -1 = the assert at :428. */
 int ots_process(ots_t *t, const float *input, float *output, size_t len) {
     size_t H = t->head_block_size, T = t->tail_block_size;
-    if (len > H) return -1;                                          /* :428 */
-    ou_process(t->head, input, output, len);                         /* :431 */
-    /* :434 tail_input.is_empty() is false for T >= 1 */
+    if (len > H) return -1;                                          /* :414 */
+    ou_process(t->head, input, output, len);                         /* :417 */
+    /* :420 tail_input.is_empty() is false for T >= 1 */
     size_t processed = 0;
-    while (processed < len) {                                        /* :441 */
+    while (processed < len) {                                        /* :427 */
         size_t remaining = len - processed;
         size_t processing = H - (t->tail_input_fill % H);
         if (remaining < processing) processing = remaining;
         size_t sb = processed, se = processed + processing;
-        {   /* :453-459 */
+        {   /* :439-445 */
             size_t p = t->precalculated_pos;
             for (size_t i = sb; i < se; i++) output[i] += t->tail_precalculated0[p++];
         }
-        {   /* :462-468 */
+        {   /* :448-454 */
             size_t p = t->precalculated_pos;
             for (size_t i = sb; i < se; i++) output[i] += t->tail_precalculated[p++];
         }
-        t->precalculated_pos += processing;                           /* :470 */
-        /* :473-474 slice panics when head does not divide T (non-power-of-two head) */
+        t->precalculated_pos += processing;                           /* :456 */
+        /* :459-460 slice panics when head does not divide T (non-power-of-two head) */
         if (t->tail_input_fill + processing > T) return -1;
         memcpy(t->tail_input + t->tail_input_fill, input + processed, processing * sizeof(float));
-        t->tail_input_fill += processing;                             /* :473-475 */
-        if (t->tail_input_fill % H == 0) {                            /* :478-490 */
+        t->tail_input_fill += processing;                             /* :459-461 */
+        if (t->tail_input_fill % H == 0) {                            /* :464-476 */
             size_t off = t->tail_input_fill - H;
             ou_process(t->tail0, t->tail_input + off, t->tail_output0 + off, H);
             if (t->tail_input_fill == T) {
@@ -478,13 +478,13 @@ int ots_process(ots_t *t, const float *input, float *output, size_t len) {
                 t->tail_output0 = s;
             }
         }
-        if (t->tail_input_fill == T) {                                /* :493-500 */
+        if (t->tail_input_fill == T) {                                /* :479-486 */
             float *s = t->tail_precalculated;
             t->tail_precalculated = t->tail_output;
             t->tail_output = s;
             ou_process(t->tail, t->tail_input, t->tail_output, T);
         }
-        if (t->tail_input_fill == T) {                                /* :502-505 */
+        if (t->tail_input_fill == T) {                                /* :488-491 */
             t->tail_input_fill = 0;
             t->precalculated_pos = 0;
         }
@@ -493,7 +493,7 @@ int ots_process(ots_t *t, const float *input, float *output, size_t len) {
     return 0;
 }
 
-/* TwoStageFFTConvolver::reset (:511-525). */
+/* TwoStageFFTConvolver::reset (:497-511). */
 void ots_reset(ots_t *t) {
     size_t T = t->tail_block_size;
     ou_reset(t->head);

@@ -91,12 +91,12 @@ def _ptr(a: np.ndarray):
 
 
 def compute_tail_block_size(head_len: int, response_len: int) -> int:
-    """src/fft_convolver.rs:534-540."""
+    """src/fft_convolver.rs:520-540."""
     return int(lib().oracle_compute_tail_block_size(head_len, response_len))
 
 
 def complex_size(n: int) -> int:
-    """src/fft_convolver.rs:66-68."""
+    """src/fft_convolver.rs:52-68."""
     return int(lib().oracle_complex_size(n))
 
 
@@ -114,7 +114,7 @@ class _Handle:
 
 
 class FFTConvolver(_Handle):
-    """src/fft_convolver.rs:100-321."""
+    """src/fft_convolver.rs:86-321."""
 
     _free = "ou_free"
 
@@ -172,7 +172,7 @@ class FFTConvolver(_Handle):
 
 
 class TwoStageFFTConvolver(_Handle):
-    """src/fft_convolver.rs:337-526."""
+    """src/fft_convolver.rs:323-526."""
 
     _free = "ots_free"
 
@@ -185,7 +185,7 @@ class TwoStageFFTConvolver(_Handle):
         return cls(h)
 
     def update(self, response):
-        raise OraclePanic("not yet implemented")  # todo!() at src/fft_convolver.rs:422-424
+        raise OraclePanic("not yet implemented")  # todo!() at src/fft_convolver.rs:408-410
 
     def reset(self):
         lib().ots_reset(self._h)

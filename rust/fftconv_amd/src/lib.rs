@@ -5,7 +5,7 @@
 //! of libfftconv_amd.so (include/fftconv.h).  Error behaviour follows the
 //! reference: where it panics (`FFTCONV_E_INVALID`) or has `todo!()`
 //! (`FFTCONV_E_UNIMPLEMENTED`) these panic with the library's message; a
-//! failed C2R (realfft's error path, src/fft_convolver.rs:278-281) zero-fills
+//! failed C2R (realfft's error path, src/fft_convolver.rs:264-267) zero-fills
 //! the output inside the library exactly as the reference does.
 //! `GpuFFTConvolverBatch` exposes the batched, HBM-resident path
 //! (`process_device`) used for throughput.
@@ -75,7 +75,7 @@ gpu_convolver!(GpuTwoStageFFTConvolver, fftconv_twostage, fftconv_twostage_init,
 gpu_convolver!(GpuCrossfadeConvolver, fftconv_crossfade, fftconv_crossfade_init, fftconv_crossfade_update,
                fftconv_crossfade_reset, fftconv_crossfade_clone, fftconv_crossfade_destroy);
 
-/// FFTConvolver (src/fft_convolver.rs:100-321).
+/// FFTConvolver (src/fft_convolver.rs:86-307).
 impl Convolution for GpuFFTConvolver {
     fn init(response: &[f32], max_block_size: usize, max_response_length: usize) -> Self {
         Self::init_raw(response, max_block_size, max_response_length)
@@ -94,7 +94,7 @@ impl Convolution for GpuFFTConvolver {
     }
 }
 
-/// TwoStageFFTConvolver (src/fft_convolver.rs:337-526); `update` is the
+/// TwoStageFFTConvolver (src/fft_convolver.rs:323-512); `update` is the
 /// reference's `todo!()` and panics the same way.
 impl Convolution for GpuTwoStageFFTConvolver {
     fn init(response: &[f32], max_block_size: usize, max_response_length: usize) -> Self {

@@ -3,8 +3,8 @@
 The path shards by channel with no data-path exchange, so a sharded run must
 reproduce the single-process run bit for bit; the only collective is the
 optional dry-block broadcast.  The oracle stands in for the GPU compute here
-(it is the checker; the HIP path is covered by the gpu tests, including a
-two-shard-vs-one bitwise check on the device)."""
+(it is the checker); tests/test_dist_gpu.py runs the same two-rank gloo job on
+the HIP library (-m gpu) and checks it bitwise against one process."""
 import os
 import socket
 

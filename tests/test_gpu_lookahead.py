@@ -1,8 +1,9 @@
 """The lookahead step (fft-convolution_amd/csrc/la.hpp) on the device.
 
-FFTConvolver::process (src/fft_convolver.rs:229-309) for a full block with
-the FDL sum re-associated in time: mid anchors sum rows 5..32 four blocks
-ahead, far anchors rows >= 33 thirty-two blocks ahead.  Checked against the oracle (tolerance REL_TOL, as every
+FFTConvolver::process (src/fft_convolver.rs:215-295) for a full block with
+the FDL sum re-associated in time: the step sums rows 1..5, mid anchors sum
+rows 6..32 five blocks ahead, far anchors rows >= 33 thirty-two blocks ahead
+(S >= 40).  Checked against the oracle (tolerance REL_TOL, as every
 parity test), and for the property the design rests on -- the summation
 order is canonical, so the bits do not depend on a channel's stagger phase,
 its index, the shard it sits in, or whether a step was served from a window

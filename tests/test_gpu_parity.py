@@ -22,7 +22,7 @@ def run_chunks(conv, x, chunks):
 # the reference's inline tests, on the device
 # ---------------------------------------------------------------------------
 def test_fft_convolver_passthrough(amd):
-    """src/fft_convolver.rs:323-335."""
+    """src/fft_convolver.rs:309-335."""
     response = np.zeros(1024, np.float32)
     response[0] = 1.0
     conv = amd.FFTConvolver.init(response, 1024, response.size)
@@ -31,7 +31,7 @@ def test_fft_convolver_passthrough(amd):
 
 
 def test_fft_twostage_convolver_passthrough(amd):
-    """src/fft_convolver.rs:542-554."""
+    """src/fft_convolver.rs:528-554."""
     response = np.zeros(1024, np.float32)
     response[0] = 1.0
     conv = amd.TwoStageFFTConvolver.init(response, 1024, response.size)
@@ -316,7 +316,7 @@ def test_uniform_batch_distinct_channels(amd, oracle_mod):
 
 
 def test_uniform_update_sequence(amd, oracle_mod):
-    """update() keeps the FDL/current/fill and zeroes overlap+pre (:188-227),
+    """update() keeps the FDL/current/fill and zeroes overlap+pre (:174-213),
     including a mid-block update and a shrinking active_seg_count."""
     rng = np.random.default_rng(11)
     B, L = 64, 1000
@@ -421,7 +421,7 @@ def test_uniform_clone(amd, oracle_mod):
 
 def test_uniform_nonfinite_zero_fills(amd, oracle_mod):
     """A NaN makes realfft's C2R fail; the reference zero-fills the output and
-    leaves fill/current where they were (src/fft_convolver.rs:278-281)."""
+    leaves fill/current where they were (src/fft_convolver.rs:264-267)."""
     rng = np.random.default_rng(14)
     B, L = 64, 500
     h = ir(rng, L)
@@ -664,7 +664,7 @@ def test_cfg2_full_size_sampled_channels(amd, oracle_mod):
 
 @pytest.mark.parametrize("B,L", [(64, 5000), (256, 40 * 256 + 5), (512, 44 * 512 - 3), (1024, 9 * 1024 + 17)])
 def test_ir_transform_wave_kernel_bitwise(amd, oracle_mod, B, L):
-    """FFTConvolver::init / update (src/fft_convolver.rs:145-156, :204-226): the
+    """FFTConvolver::init / update (src/fft_convolver.rs:131-142, :190-212): the
     IR segment transforms one per wave (default, 64 <= B <= 1024) give the same
     spectra bits as one per workgroup (variant bit 7), through init, an update
     to a shorter response (zeroed rows) and back; and match the oracle."""

@@ -1,6 +1,6 @@
 """Pins the oracle (oracle/fftconv_oracle.c) before it is trusted as the GPU
 checker: the reference's own known-answer and self-consistency tests
-(src/tests.rs, src/fft_convolver.rs:323-335/542-554,
+(src/tests.rs, src/fft_convolver.rs:309-321/542-554,
 src/crossfade_convolver.rs:107-124/281-316) run against it, plus the
 independent f64 direct convolution that UPOLS must equal.
 CPU only."""
@@ -171,7 +171,7 @@ def test_twostage_equals_f64_convolution(oracle_mod, head, L):
 
 def test_twostage_non_power_of_two_head_panics(oracle_mod):
     """head 48 does not divide T = 512: tail_input[fill..fill+48] runs past T
-    on the 11th block and the reference panics (src/fft_convolver.rs:473-474)."""
+    on the 11th block and the reference panics (src/fft_convolver.rs:459-460)."""
     conv = oracle_mod.TwoStageFFTConvolver.init(np.ones(5000, np.float32), 48, 5000)
     assert conv.tail_block_size == 512
     for _ in range(10):
