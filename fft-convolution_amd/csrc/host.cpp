@@ -120,6 +120,89 @@ struct Scratch {
     }
 };
 
+// Cross-stream ordering of one handle's work.  Asynchronous entry points take
+// a caller stream; every call must still see the state the previous call left
+// (the reference's calls are sequential on one instance).  `enter(s)` before
+// enqueueing on s makes s wait for the stream of the handle's previous work
+// when that was another stream (an event recorded there now -- so, as with a
+// library handle's stream, a caller stream must stay valid until the handle's
+// next call).  Host-synchronous entry points enter their own stream and wait
+// for it alone: no device-wide synchronisation, so other handles' and other
+// libraries' streams are never waited for.
+struct StreamOrder {
+    hipStream_t last = nullptr;
+    bool any = false;
+    hipEvent_t ev = nullptr;
+    ~StreamOrder() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    int enter(hipStream_t s) {
+        if (any && last != s) {
+            if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(ev, last));
+            HIP_TRY(hipStreamWaitEvent(s, ev, 0));
+        }
+        last = s;
+        any = true;
+        return FFTCONV_OK;
+    }
+    // every piece of the handle's work has finished, once `own` has drained
+    int drain(hipStream_t own) {
+        if (int r = enter(own)) return r;
+        HIP_TRY(hipStreamSynchronize(own));
+        return FFTCONV_OK;
+    }
+};
+
+// Pinned host staging for host-memory IR uploads: update() copies the caller's
+// response into it and returns once the H2D copy and the IR transform are
+// enqueued (the next call on the handle is ordered behind them).  Reserved at
+// init, so update() never allocates (src/lib.rs:8); `busy` guards its reuse.
+struct PinnedStage {
+    float *p = nullptr;
+    size_t n = 0;
+    hipEvent_t busy = nullptr;
+    bool pending = false;
+    PinnedStage() = default;
+    PinnedStage(const PinnedStage &) = delete;
+    PinnedStage &operator=(const PinnedStage &) = delete;
+    ~PinnedStage() {
+        if (busy) {
+            if (pending) (void)hipEventSynchronize(busy);
+            (void)hipEventDestroy(busy);
+        }
+        if (p) (void)hipHostFree(p);
+    }
+    int alloc(size_t count) {
+        if (count == 0) return FFTCONV_OK;
+        hipError_t e = hipHostMalloc((void **)&p, count * sizeof(float), hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(FFTCONV_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        }
+        n = count;
+        HIP_TRY(hipEventCreateWithFlags(&busy, hipEventDisableTiming));
+        return FFTCONV_OK;
+    }
+    // wait until the previous upload has left the buffer (normally long done)
+    int acquire() {
+        if (pending) HIP_TRY(hipEventSynchronize(busy));
+        pending = false;
+        return FFTCONV_OK;
+    }
+    int release(hipStream_t s) {  // after the H2D copy out of the buffer is enqueued on s
+        HIP_TRY(hipEventRecord(busy, s));
+        pending = true;
+        return FFTCONV_OK;
+    }
+    // channel c of the caller's responses (src + c*stride, len samples) to
+    // rows of `row` floats; stride 0 = one response for every channel (1 row)
+    void fill(const float *src, size_t nch, size_t len, size_t stride, size_t row) {
+        const size_t rows = stride == 0 ? 1 : nch;
+        for (size_t c = 0; c < rows; ++c) std::memcpy(p + c * row, src + c * stride, len * sizeof(float));
+    }
+};
+
 // ---------------------------------------------------------------------------
 // UniformCore -- a batch of FFTConvolver instances
 // ---------------------------------------------------------------------------
@@ -135,6 +218,8 @@ struct UniformCore {
     DevPtr<int4> state;
     hipStream_t stream = nullptr;
     Scratch scratch;
+    PinnedStage hstage;            // host IR uploads (update_host), [C][ir_len]
+    mutable StreamOrder order;     // (clone_from drains its source)
     // lookahead (la.hpp): standalone batches only (la_ok, set before init)
     bool la_ok = false;
     int la_W = 0;                 // far parts (partial rows per step), 0 = off
@@ -146,7 +231,7 @@ struct UniformCore {
     ~UniformCore() {
         if (stream) {
             DeviceGuard g(device);
-            (void)hipStreamSynchronize(stream);
+            (void)order.drain(stream);  // (work still queued on a caller stream reads these buffers)
             (void)hipStreamDestroy(stream);
         }
     }
@@ -171,6 +256,7 @@ struct UniformCore {
         if (int r = state.alloc(C)) return r;
         if (int r = tw.alloc(2 * B)) return r;
         if (int r = staging.alloc(C * ir_len)) return r;  // update() never allocates
+        if (int r = hstage.alloc(C * ir_len)) return r;
         la_W = la_ok ? la_parts(log2b, (int)S) : 0;
         if (la_W) {
             const LaDims d = la_dims(log2b);
@@ -250,12 +336,24 @@ struct UniformCore {
         if (len > ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
         if (ir_len == 0) return FFTCONV_OK;                        // :181-183
         DeviceGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());  // work may be in flight on a caller stream
-        if (int r = upload(chan0, nch, src, len, stride, stream)) return r;
+        // asynchronous: the response goes through the pinned stage; the copy
+        // and the transform are enqueued behind the handle's previous work,
+        // and every later call is ordered behind them (StreamOrder)
+        if (int r = order.enter(stream)) return r;
+        return update_host_on(chan0, nch, src, len, stride, stream);
+    }
+    // (the caller has ordered stream s behind the handle's previous work)
+    int update_host_on(size_t chan0, size_t nch, const float *src, size_t len, size_t stride, hipStream_t s) {
+        if (len > ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
+        if (ir_len == 0) return FFTCONV_OK;
+        if (int r = hstage.acquire()) return r;
         const size_t sst = (stride == 0 && nch > 1) ? 0 : ir_len;
-        if (int r = ir_from_device(chan0, nch, staging.p + chan0 * ir_len, sst, len, len, true, stream)) return r;
-        HIP_TRY(hipStreamSynchronize(stream));
-        return FFTCONV_OK;
+        if (len && nch) {
+            hstage.fill(src, nch, len, stride == 0 && nch > 1 ? 0 : stride, ir_len);
+            if (int r = upload(chan0, sst ? nch : 1, hstage.p, len, ir_len, s)) return r;
+            if (int r = hstage.release(s)) return r;
+        }
+        return ir_from_device(chan0, nch, staging.p + chan0 * ir_len, sst, len, len, true, s);
     }
 
     // update() from device samples, stream-ordered (used by the crossfade swap)
@@ -331,7 +429,7 @@ struct UniformCore {
         if (in_len < out_len) return fail(FFTCONV_E_INVALID, "input slice shorter than output (range end index out of range)");
         if (out_len == 0 || C == 0) return FFTCONV_OK;
         DeviceGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = order.enter(stream)) return r;
         if (int r = scratch.ensure(C * out_len, C * out_len)) return r;
         HIP_TRY(hipMemcpy2DAsync(scratch.in.p, out_len * sizeof(float), in, in_len * sizeof(float),
                                  out_len * sizeof(float), C, hipMemcpyHostToDevice, stream));
@@ -344,7 +442,7 @@ struct UniformCore {
     // #[derive(Clone)]
     int clone_from(const UniformCore &o) {
         DeviceGuard g(o.device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = o.order.drain(o.stream)) return r;
         device = o.device;
         C = o.C; ir_len = o.ir_len; B = o.B; log2b = o.log2b; S = o.S;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -364,6 +462,7 @@ struct UniformCore {
         if (int r = cp(laPm, o.laPm)) return r;
         la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
         if (int r = staging.alloc(o.staging.n)) return r;
+        if (int r = hstage.alloc(o.hstage.n)) return r;
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -371,7 +470,7 @@ struct UniformCore {
     int channel_state(size_t c, size_t out3[3]) {
         if (c >= C) return fail(FFTCONV_E_INVALID, "channel out of range");
         DeviceGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = order.drain(stream)) return r;
         int4 st;
         HIP_TRY(hipMemcpy(&st, state.p + c, sizeof(int4), hipMemcpyDeviceToHost));
         out3[0] = (size_t)st.x; out3[1] = (size_t)st.y; out3[2] = (size_t)st.z;
@@ -400,16 +499,26 @@ struct TwoStageCore {
     hipEvent_t ev_main = nullptr, ev_tail = nullptr;
     bool tail_in_flight = false;
     Scratch scratch;
+    mutable StreamOrder order;
 
     ~TwoStageCore() {
         DeviceGuard g(device);
         if (side) { (void)hipStreamSynchronize(side); (void)hipStreamDestroy(side); }
-        if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
+        if (stream) { (void)order.drain(stream); (void)hipStreamDestroy(stream); }
         if (ev_main) (void)hipEventDestroy(ev_main);
         if (ev_tail) (void)hipEventDestroy(ev_tail);
     }
 
     float *tail_input() const { return tin_buf[tin_idx].p; }
+
+    // every piece of the handle's work has finished: the caller-stream work
+    // (StreamOrder) and the tail convolution on the side stream
+    int quiesce() const {
+        if (int r = order.enter(stream)) return r;
+        if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(stream, ev_tail, 0));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
 
     // The side stream is confined to the first ncu/k CUs (k =
     // FFTCONV_TAIL_CU_DIV, default 3): a T-block tail workgroup fills a whole
@@ -588,7 +697,7 @@ struct TwoStageCore {
         if (len > head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
         if (len == 0 || C == 0) return FFTCONV_OK;
         DeviceGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = order.enter(stream)) return r;
         if (int r = scratch.ensure(C * len, C * len)) return r;
         HIP_TRY(hipMemcpyAsync(scratch.in.p, in, C * len * sizeof(float), hipMemcpyHostToDevice, stream));
         if (int r = process_device(scratch.in.p, len, scratch.out.p, len, len, stream)) return r;
@@ -599,7 +708,7 @@ struct TwoStageCore {
 
     int reset() {  // :497-511
         DeviceGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = quiesce()) return r;
         if (int r = head->reset(stream)) return r;
         if (tail0) { if (int r = tail0->reset(stream)) return r; }
         if (tail) { if (int r = tail->reset(stream)) return r; }
@@ -614,7 +723,7 @@ struct TwoStageCore {
 
     int clone_from(const TwoStageCore &o) {
         DeviceGuard g(o.device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = o.quiesce()) return r;
         device = o.device; C = o.C; head_bs = o.head_bs; T = o.T;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         auto cl = [&](std::unique_ptr<UniformCore> &dst, const std::unique_ptr<UniformCore> &src) -> int {
@@ -721,6 +830,8 @@ struct CrossfadeCore {
     // ahead of B and the crossfader did not advance.  Every later call fails
     // instead of silently mixing convolvers that are out of step.
     bool poisoned = false;
+    mutable StreamOrder order;
+    PinnedStage hstage;  // host responses for the pending path (stored_response)
     int check_poisoned() const {
         return poisoned ? fail(FFTCONV_E_DEVICE, "crossfade handle unusable: an earlier process() failed between "
                                                   "its two convolvers' launches")
@@ -730,7 +841,7 @@ struct CrossfadeCore {
     ~CrossfadeCore() {
         if (stream) {
             DeviceGuard g(device);
-            (void)hipStreamSynchronize(stream);
+            (void)order.drain(stream);
             (void)hipStreamDestroy(stream);
         }
     }
@@ -762,6 +873,7 @@ struct CrossfadeCore {
         stored_stride = stored_len;
         if (int r = stored.alloc(C * stored_len)) return r;
         if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), stream));
+        if (int r = hstage.alloc(C * stored_len)) return r;
         xf.init(crossfade_samples, std::min(mbs, max_response_length));
         max_buffer_size = mbs;
         if (int r = buf_a.alloc(C * mbs)) return r;
@@ -796,15 +908,17 @@ struct CrossfadeCore {
         if (act[0] < 0 || act[0] != act[1]) pair_ok = false;
     }
 
-    // Convolution::update (:51-64); host samples, channel c at src + c*stride (stride 0 = shared)
+    // Convolution::update (:51-64); host samples, channel c at src + c*stride
+    // (stride 0 = shared).  Asynchronous like FFTConvolver's: the response is
+    // staged in pinned memory and the work enqueued behind the handle's.
     int update_host(const float *src, size_t len, size_t stride) {
         if (int r = check_poisoned()) return r;
         DeviceGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = order.enter(stream)) return r;
         if (!is_crossfading()) {
             UniformCore &t = xf.target == 0 ? *b : *a;
             if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
-            if (int r = t.update_host(0, C, src, len, stride)) return r;
+            if (int r = t.update_host_on(0, C, src, len, stride, stream)) return r;
             note_update(xf.target == 0 ? 1 : 0, len);
             xf.fade_into(xf.target == 0 ? 1 : 0);
             response_pending = false;
@@ -814,16 +928,19 @@ struct CrossfadeCore {
         // stored_response[..len] = response; stored_response[len..] = 0
         if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), stream));
         if (len) {
-            if (stride == 0 || C == 1) {
-                HIP_TRY(hipMemcpyAsync(stored.p, src, len * sizeof(float), hipMemcpyHostToDevice, stream));
+            if (int r = hstage.acquire()) return r;
+            const bool shared = stride == 0 || C == 1;
+            hstage.fill(src, C, len, shared ? 0 : stride, stored_len);
+            if (shared) {
+                HIP_TRY(hipMemcpyAsync(stored.p, hstage.p, len * sizeof(float), hipMemcpyHostToDevice, stream));
                 stored_stride = C == 1 ? stored_len : 0;
             } else {
-                HIP_TRY(hipMemcpy2DAsync(stored.p, stored_len * sizeof(float), src, stride * sizeof(float),
+                HIP_TRY(hipMemcpy2DAsync(stored.p, stored_len * sizeof(float), hstage.p, stored_len * sizeof(float),
                                          len * sizeof(float), C, hipMemcpyHostToDevice, stream));
                 stored_stride = stored_len;
             }
+            if (int r = hstage.release(stream)) return r;
         }
-        HIP_TRY(hipStreamSynchronize(stream));
         response_pending = true;
         return FFTCONV_OK;
     }
@@ -931,7 +1048,7 @@ struct CrossfadeCore {
         if (out_len > max_buffer_size) return fail(FFTCONV_E_INVALID, "output longer than max_buffer_size (index out of bounds)");
         if (C == 0) return FFTCONV_OK;
         DeviceGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = order.enter(stream)) return r;
         const size_t m = max_buffer_size;
         if (int r = scratch.ensure(C * m, C * std::max<size_t>(out_len, 1))) return r;
         if (m)
@@ -947,7 +1064,7 @@ struct CrossfadeCore {
 
     int clone_from(const CrossfadeCore &o) {
         DeviceGuard g(o.device);
-        HIP_TRY(hipDeviceSynchronize());
+        if (int r = o.order.drain(o.stream)) return r;
         device = o.device; C = o.C; max_buffer_size = o.max_buffer_size;
         stored_len = o.stored_len; stored_stride = o.stored_stride;
         xf = o.xf; response_pending = o.response_pending;
@@ -962,6 +1079,7 @@ struct CrossfadeCore {
         if (int r = buf_b.alloc(o.buf_b.n)) return r;
         if (int r = mix_tab.alloc(o.mix_tab.n)) return r;
         if (int r = stored.alloc(o.stored.n)) return r;
+        if (int r = hstage.alloc(o.hstage.n)) return r;
         if (stored.n) HIP_TRY(hipMemcpyAsync(stored.p, o.stored.p, stored.bytes(), hipMemcpyDeviceToDevice, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
@@ -1066,12 +1184,14 @@ int fftconv_uniform_update_device(fftconv_uniform *h, const float *d_responses, 
                                   void *hip_stream) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    return h->core.update_device(d_responses, h->core.C == 1 ? 0 : stride, len, pick(hip_stream, h->core.stream));
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
+    return h->core.update_device(d_responses, h->core.C == 1 ? 0 : stride, len, s);
 }
 int fftconv_uniform_reset(fftconv_uniform *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    HIP_TRY(hipDeviceSynchronize());
+    if (int r = h->core.order.enter(h->core.stream)) return r;
     if (int r = h->core.reset(h->core.stream)) return r;
     HIP_TRY(hipStreamSynchronize(h->core.stream));
     return FFTCONV_OK;
@@ -1085,7 +1205,9 @@ int fftconv_uniform_process_device(fftconv_uniform *h, const float *d_input, siz
                                    size_t out_stride, size_t len, void *hip_stream) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    return h->core.process_device(d_input, in_stride, d_output, out_stride, len, pick(hip_stream, h->core.stream));
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
+    return h->core.process_device(d_input, in_stride, d_output, out_stride, len, s);
 }
 int fftconv_uniform_process_device_steps(fftconv_uniform *h, const float *d_input, size_t in_stride, size_t in_step,
                                    float *d_output, size_t out_stride, size_t out_step, size_t len, size_t steps,
@@ -1093,6 +1215,7 @@ int fftconv_uniform_process_device_steps(fftconv_uniform *h, const float *d_inpu
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
     hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
     for (size_t k = 0; k < steps; ++k) {
         if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
             return r;
@@ -1109,8 +1232,7 @@ void fftconv_uniform_destroy(fftconv_uniform *h) { delete h; }
 int fftconv_uniform_synchronize(fftconv_uniform *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    HIP_TRY(hipStreamSynchronize(h->core.stream));
-    return FFTCONV_OK;
+    return h->core.order.drain(h->core.stream);
 }
 size_t fftconv_uniform_channels(const fftconv_uniform *h) { return h ? h->core.C : 0; }
 int fftconv_uniform_lookahead_parts(const fftconv_uniform *h) { return h ? h->core.la_W : 0; }
@@ -1153,7 +1275,9 @@ int fftconv_twostage_process_device(fftconv_twostage *h, const float *d_input, s
                                     size_t out_stride, size_t len, void *hip_stream) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    return h->core.process_device(d_input, in_stride, d_output, out_stride, len, pick(hip_stream, h->core.stream));
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
+    return h->core.process_device(d_input, in_stride, d_output, out_stride, len, s);
 }
 int fftconv_twostage_process_device_steps(fftconv_twostage *h, const float *d_input, size_t in_stride, size_t in_step,
                                    float *d_output, size_t out_stride, size_t out_step, size_t len, size_t steps,
@@ -1161,6 +1285,7 @@ int fftconv_twostage_process_device_steps(fftconv_twostage *h, const float *d_in
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
     hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
     for (size_t k = 0; k < steps; ++k) {
         if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
             return r;
@@ -1177,8 +1302,7 @@ void fftconv_twostage_destroy(fftconv_twostage *h) { delete h; }
 int fftconv_twostage_synchronize(fftconv_twostage *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    HIP_TRY(hipStreamSynchronize(h->core.stream));
-    return FFTCONV_OK;
+    return h->core.quiesce();
 }
 size_t fftconv_twostage_tail_block_size(const fftconv_twostage *h) { return h ? h->core.T : 0; }
 
@@ -1220,7 +1344,9 @@ int fftconv_crossfade_update_device(fftconv_crossfade *h, const float *d_respons
                                     void *hip_stream) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    return h->core.update_device(d_responses, len, h->core.C == 1 ? 0 : stride, pick(hip_stream, h->core.stream));
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
+    return h->core.update_device(d_responses, len, h->core.C == 1 ? 0 : stride, s);
 }
 int fftconv_crossfade_reset(fftconv_crossfade *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
@@ -1235,8 +1361,9 @@ int fftconv_crossfade_process_device(fftconv_crossfade *h, const float *d_input,
                                      size_t out_stride, size_t output_len, void *hip_stream) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    return h->core.process_device(d_input, in_stride, d_output, out_stride, output_len,
-                                  pick(hip_stream, h->core.stream));
+    hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
+    return h->core.process_device(d_input, in_stride, d_output, out_stride, output_len, s);
 }
 int fftconv_crossfade_is_crossfading(const fftconv_crossfade *h) { return h && h->core.is_crossfading() ? 1 : 0; }
 int fftconv_crossfade_process_device_steps(fftconv_crossfade *h, const float *d_input, size_t in_stride, size_t in_step,
@@ -1245,6 +1372,7 @@ int fftconv_crossfade_process_device_steps(fftconv_crossfade *h, const float *d_
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
     hipStream_t s = pick(hip_stream, h->core.stream);
+    if (int r = h->core.order.enter(s)) return r;
     for (size_t k = 0; k < steps; ++k) {
         if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
             return r;
@@ -1261,8 +1389,7 @@ void fftconv_crossfade_destroy(fftconv_crossfade *h) { delete h; }
 int fftconv_crossfade_synchronize(fftconv_crossfade *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    HIP_TRY(hipStreamSynchronize(h->core.stream));
-    return FFTCONV_OK;
+    return h->core.order.drain(h->core.stream);
 }
 
 }  // extern "C"
