@@ -295,7 +295,29 @@ struct UniformCore {
         a.len_data = (long long)len_data; a.len_active = (long long)len_active;
         a.tw = tw.p; a.S = (int)S; a.chan0 = (int)chan0; a.update_state = update_state ? 1 : 0;
         HIP_TRY(launch_ir_segments(log2b, a, (int)nch, s));
-        if (update_state) la_all = true;  // the updated channels dropped their windows
+        // the updated channels dropped their windows: rebuild them now, in
+        // the update, so the next process launch stays a steady-state one
+        if (update_state && !la_all) return la_rebuild(s, chan0, nch);
+        return FFTCONV_OK;
+    }
+
+    // lookahead windows of channels [chan0, chan0+nch) from the current H and
+    // FDL (launch_la_rebuild), as if anchored by the launch before the next
+    // one; without the lookahead step (or with VARIANT_LAFULL) nothing to do
+    int la_rebuild(hipStream_t s, size_t chan0, size_t nch) {
+        if (!la_W || la_parts(log2b, (int)S) != la_W || la_full_variant() || nch == 0) return FFTCONV_OK;
+        const LaDims d = la_dims(log2b);
+        const unsigned long long per = (unsigned long long)(d.DF * d.DM);
+        ProcArgs a{};
+        a.job[0] = job(nullptr, 0, nullptr, 0, B);
+        a.tw = tw.p;
+        a.njobs = 1;
+        a.laP = laP.p;
+        a.laPm = laPm.p;
+        a.la_W = la_W;
+        a.la_c0 = (int)chan0;
+        a.la_t = (int)((la_t + per - 1) % per);
+        HIP_TRY(launch_la_rebuild(log2b, a, (int)(chan0 + nch), s));
         return FFTCONV_OK;
     }
 
@@ -326,6 +348,10 @@ struct UniformCore {
             // every channel reads its own staging row; a shared response reads row 0
             const size_t sst = (stride == 0 && C > 1) ? 0 : ir_len;
             if (int r = ir_from_device(0, C, staging.p, sst, len, ir_len, false, stream)) return r;
+        }
+        if (la_W && !la_full_variant()) {  // the first process launch is a steady-state one too
+            if (int r = la_rebuild(stream, 0, C)) return r;
+            la_all = false;
         }
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
@@ -369,6 +395,10 @@ struct UniformCore {
         if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), s));
         if (pre.n) HIP_TRY(hipMemsetAsync(pre.p, 0, pre.bytes(), s));
         HIP_TRY(launch_reset_state(state.p, (int)C, s));
+        if (la_W && !la_full_variant()) {  // windows of the zeroed FDL, in the reset
+            la_all = false;
+            return la_rebuild(s, 0, C);
+        }
         la_all = true;
         return FFTCONV_OK;
     }

@@ -1411,6 +1411,78 @@ hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStre
     FFTCONV_DISPATCH(launch_la_t, log2b, a, channels, s)
 }
 
+// ---------------------------------------------------------------------------
+// Window rebuild after update() / reset / init (FFTConvolver::update
+// :174-213 keeps the FDL but replaces H, so every partial-sum window is
+// stale).  Instead of the next process launch re-anchoring every channel on
+// its latency-critical path, the update enqueues this anchors-only launch:
+// each channel's far and mid windows, as the anchors of the previous launch
+// would have left them (la_anchor_state, la_rebuild), then the state words
+// pointing at them.  The next process launch is a steady-state launch.
+// ---------------------------------------------------------------------------
+template <int LOG2B, bool NTL>
+__global__ __launch_bounds__(LA_NT, 4) void la_rebuild_kernel(ProcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int b = (int)blockIdx.x;
+    if (b < a.la_nfar) la_anchor_far<LOG2B, NTL>(a, b, smem);
+    else la_anchor_mid<LOG2B, NTL>(a, b - a.la_nfar);
+}
+
+// the state words of the rebuilt windows (same eligibility test as the
+// anchors: both read the state word the update left)
+template <int LOG2B>
+__global__ void la_rebuild_state_kernel(ProcArgs a) {
+    const int c = a.la_c0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (c >= a.la_channels) return;
+    const int4 st = a.job[0].state[c];
+    if (!la_eligible<LOG2B>(st, a.job[0].n)) return;
+    int nf = st.w & ~(LA_MASK | SEQ_MASK);  // (launch tag 0: no process launch wrote it)
+    // (the anchors wrote the other window of each level: toggle its flag)
+    nf = (nf ^ FLAG_PWIN) | FLAG_LA | ((la_dnew(c, a, LA_DF) - 1) << LA_D_SHIFT);
+    nf = (nf ^ FLAG_PWINM) | FLAG_LAM | ((la_dnew(c, a, LA_DM) - 1) << LA_DM_SHIFT);
+    a.job[0].state[c].w = nf;
+}
+
+template <int LOG2B>
+static hipError_t launch_rebuild_t(const ProcArgs &a, int channels, hipStream_t s) {
+    if constexpr (LOG2B < 7 || LOG2B > 9) {
+        return hipErrorNotSupported;
+    } else {
+        using LG = LaGeo<LOG2B>;
+        constexpr size_t lds = (LG::anchor_bytes + 15) / 16 * 16 + 16;
+        if (a.la_W != LG::WF || !a.laPm || !a.laP || a.njobs != 1 || a.job[0].n != (1 << LOG2B))
+            return hipErrorInvalidValue;
+        const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
+        const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
+        auto kern = ntl ? la_rebuild_kernel<LOG2B, true> : la_rebuild_kernel<LOG2B, false>;
+        ProcArgs args = a;
+        args.la_channels = channels;
+        args.la_all = 1;
+        args.la_rebuild = 1;
+        args.la_seq = 0;
+        args.la_probe = 0;
+        const int nch = channels - a.la_c0;
+        if (nch <= 0) return hipSuccess;
+        args.la_nfar = (nch + 7) / 8 * 8 * LG::WG_FAR;
+        args.la_nmid = nch;
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(kern, dim3(args.la_nfar + args.la_nmid), dim3(LA_NT), lds, s, args);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        hipLaunchKernelGGL(la_rebuild_state_kernel<LOG2B>, dim3((nch + 255) / 256), dim3(256), 0, s, args);
+        return hipGetLastError();
+    }
+}
+
+hipError_t launch_la_rebuild(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    FFTCONV_DISPATCH(launch_rebuild_t, log2b, a, channels, s)
+}
+
+bool la_full_variant() { return g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL); }
+
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s) {
     if (channels <= 0 || a.S <= 0) return hipSuccess;
     FFTCONV_DISPATCH(launch_ir_t, log2b, a, channels, s)

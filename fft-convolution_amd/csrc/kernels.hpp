@@ -110,6 +110,11 @@ struct ProcArgs {
     // 2 = B's launch mixes in its epilogue: out = mix(mix.buf_a, B's block)
     int la_mix;
     float *mix_tab;        // [n] mix_selector of each sample (la_mix 1 writes, 2 reads)
+    // window rebuild (launch_la_rebuild, after update / reset / init): anchors
+    // only, for channels [la_c0, la_channels), as if they had run in the
+    // launch before the next one (la_t = that launch's counter)
+    int la_rebuild;
+    int la_c0;
 };
 
 struct IrArgs {
@@ -163,6 +168,10 @@ struct LaDims {
 };
 LaDims la_dims(int log2b);
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s);
+// every far and mid window of channels [a.la_c0, channels) rebuilt from the
+// current H and FDL (anchors only), then their state words pointed at them
+hipError_t launch_la_rebuild(int log2b, const ProcArgs &a, int channels, hipStream_t s);
+bool la_full_variant();  // VARIANT_LAFULL: lookahead launches without anchors
 
 constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)
 

@@ -261,6 +261,17 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int c, int P,
     const int sz = __builtin_amdgcn_readfirstlane(st.z), sw = __builtin_amdgcn_readfirstlane(st.w);
     const bool far = P == LA_DF;
     act = sy;
+    if (a.la_rebuild) {
+        // window rebuild (no steps in this launch): the window an anchor of
+        // the previous launch would have opened, i.e. as after that launch's
+        // step -- window step 0 serves the next step (current = sx), whose
+        // row i meets FDL row (sx + i) % act = age i - 1 from sx + 1
+        if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return false;
+        cur = sx + 1 == act ? 0 : sx + 1;
+        win = (sw & (far ? FLAG_PWIN : FLAG_PWINM)) ? 0 : 1;
+        d = la_dnew(c, a, P);
+        return true;
+    }
     if (((sw & SEQ_MASK) >> SEQ_SHIFT) == a.la_seq) {
         // this launch's step has already stored the channel's state: it
         // opened a window iff the state says so (j = 0)
@@ -292,10 +303,11 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
     // then serves the rows the window halves and neighbouring groups share
     const int x = b & 7, y = b >> 3;
     const int ci = (y / LG::WG_FAR) * 8 + x, r = y % LG::WG_FAR;
-    const int c = a.la_all > 0 ? ci : (a.la_t % LA_DF) + LA_DF * ci;
+    const int c = a.la_all > 0 ? a.la_c0 + ci : (a.la_t % LA_DF) + LA_DF * ci;
     if (c >= a.la_channels) return;  // (padding of the last XCD round)
     int cur, act, win, d;
     if (!la_anchor_state<LOG2B>(a, c, LA_DF, cur, act, win, d)) return;
+    if ((r / (LG::NSL * LG::WF)) * LA_JW >= d) return;  // a window slice wholly past the window
 
     constexpr int FS = LG::FS, NSL = LG::NSL;
     const int tid = threadIdx.x;
@@ -351,7 +363,7 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
     using LG = LaGeo<LOG2B>;
     constexpr int B = LG::B, F = LG::F, JM = LG::JM;
     const ProcJob &J = a.job[0];
-    const int c = a.la_all > 0 ? b : (a.la_t % LA_DM) + LA_DM * b;
+    const int c = a.la_all > 0 ? a.la_c0 + b : (a.la_t % LA_DM) + LA_DM * b;
     if (c >= a.la_channels) return;
     int cur, act, win, d;
     if (!la_anchor_state<LOG2B>(a, c, LA_DM, cur, act, win, d)) return;

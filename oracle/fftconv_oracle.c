@@ -711,7 +711,8 @@ static float urand(uint64_t *s) { /* U[-1, 1) */
 }
 
 typedef struct {
-    size_t c0, c1, block, ir_len, nblocks, warm;
+    int kind; /* 0 FFTConvolver, 1 TwoStageFFTConvolver (block = head), 2 CrossfadeConvolver */
+    size_t c0, c1, block, ir_len, nblocks, warm, every;
     uint64_t seed;
     double secs;
     int err;
@@ -723,51 +724,74 @@ static double now_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+/* One instance per channel (the reference is one instance per channel), each
+ * fed its own white-noise block every call.  kind 2 swaps in a fresh response
+ * on every channel every `every` blocks (update(), timed like process()). */
 static void *bench_worker(void *arg) {
     bench_job_t *j = (bench_job_t *)arg;
     size_t nc = j->c1 - j->c0;
-    ou_t **cv = (ou_t **)calloc(nc ? nc : 1, sizeof(ou_t *));
+    void **cv = (void **)calloc(nc ? nc : 1, sizeof(void *));
     float *ir = (float *)malloc(j->ir_len * sizeof(float));
+    float *ir2 = (float *)malloc(j->ir_len * sizeof(float));
     float *in = (float *)malloc(nc * j->block * sizeof(float) + 4);
     float *out = (float *)malloc(j->block * sizeof(float));
-    if (!cv || !ir || !in || !out) { j->err = 1; goto done; }
+    if (!cv || !ir || !ir2 || !in || !out) { j->err = 1; goto done; }
     float g = 1.0f / sqrtf((float)j->ir_len);
     for (size_t c = 0; c < nc; c++) {
         uint64_t s = j->seed + (j->c0 + c) * 7919u;
         for (size_t i = 0; i < j->ir_len; i++) ir[i] = urand(&s) * g;
-        cv[c] = ou_init(ir, j->ir_len, j->block, j->ir_len);
+        cv[c] = j->kind == 0 ? (void *)ou_init(ir, j->ir_len, j->block, j->ir_len)
+              : j->kind == 1 ? (void *)ots_init(ir, j->ir_len, j->block, j->ir_len)
+                             : (void *)ocf_init(ir, j->ir_len, j->block, j->ir_len);
         if (!cv[c]) { j->err = 1; goto done; }
         for (size_t i = 0; i < j->block; i++) in[c * j->block + i] = urand(&s);
     }
-    for (size_t b = 0; b < j->warm; b++)
-        for (size_t c = 0; c < nc; c++) ou_process(cv[c], in + c * j->block, out, j->block);
-    double t0 = now_s();
+    uint64_t s2 = j->seed ^ 0x5bd1e995u;
+    for (size_t i = 0; i < j->ir_len; i++) ir2[i] = urand(&s2) * g;
     volatile float sink = 0.0f;
-    for (size_t b = 0; b < j->nblocks; b++)
+    double t0 = 0.0;
+    for (size_t b = 0; b < j->warm + j->nblocks; b++) {
+        if (b == j->warm) t0 = now_s();
         for (size_t c = 0; c < nc; c++) {
-            ou_process(cv[c], in + c * j->block, out, j->block);
+            const float *x = in + c * j->block;
+            if (j->kind == 0) {
+                ou_process((ou_t *)cv[c], x, out, j->block);
+            } else if (j->kind == 1) {
+                if (ots_process((ots_t *)cv[c], x, out, j->block)) j->err = 1;
+            } else {
+                if (j->every && b % j->every == j->every - 1) ocf_update((ocf_t *)cv[c], (b / j->every) & 1 ? ir : ir2, j->ir_len);
+                if (ocf_process((ocf_t *)cv[c], x, j->block, out, j->block)) j->err = 1;
+            }
             sink += out[0];
         }
+    }
     j->secs = now_s() - t0;
 done:
-    if (cv) for (size_t c = 0; c < nc; c++) ou_free(cv[c]);
-    free(cv); free(ir); free(in); free(out);
+    if (cv)
+        for (size_t c = 0; c < nc; c++) {
+            if (!cv[c]) continue;
+            if (j->kind == 0) ou_free((ou_t *)cv[c]);
+            else if (j->kind == 1) ots_free((ots_t *)cv[c]);
+            else ocf_free((ocf_t *)cv[c]);
+        }
+    free(cv); free(ir); free(ir2); free(in); free(out);
     return NULL;
 }
 
 /* Returns the wall seconds of the timed region (max over threads), < 0 on error. */
-double oracle_bench_uniform(size_t channels, size_t block, size_t ir_len, size_t nblocks,
-                            size_t warm, size_t threads, uint64_t seed) {
+double oracle_bench(int kind, size_t channels, size_t block, size_t ir_len, size_t nblocks, size_t warm,
+                    size_t threads, uint64_t seed, size_t every) {
     if (threads < 1) threads = 1;
     if (threads > channels) threads = channels;
     pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
     bench_job_t *jobs = (bench_job_t *)calloc(threads, sizeof(bench_job_t));
     if (!th || !jobs) { free(th); free(jobs); return -1.0; }
     for (size_t t = 0; t < threads; t++) {
+        jobs[t].kind = kind;
         jobs[t].c0 = channels * t / threads;
         jobs[t].c1 = channels * (t + 1) / threads;
         jobs[t].block = block; jobs[t].ir_len = ir_len; jobs[t].nblocks = nblocks;
-        jobs[t].warm = warm; jobs[t].seed = seed;
+        jobs[t].warm = warm; jobs[t].seed = seed; jobs[t].every = every;
         pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
     }
     double worst = 0.0;
@@ -779,4 +803,9 @@ double oracle_bench_uniform(size_t channels, size_t block, size_t ir_len, size_t
     }
     free(th); free(jobs);
     return err ? -1.0 : worst;
+}
+
+double oracle_bench_uniform(size_t channels, size_t block, size_t ir_len, size_t nblocks,
+                            size_t warm, size_t threads, uint64_t seed) {
+    return oracle_bench(0, channels, block, ir_len, nblocks, warm, threads, seed, 0);
 }

@@ -73,6 +73,7 @@ def lib():
             "oracle_xfader_mix": (C.c_float, [vp, C.c_float, C.c_float]),
             "oracle_xfader_state": (C.c_int, [vp]),
             "oracle_bench_uniform": (C.c_double, [_sz, _sz, _sz, _sz, _sz, _sz, C.c_uint64]),
+            "oracle_bench": (C.c_double, [C.c_int, _sz, _sz, _sz, _sz, _sz, _sz, C.c_uint64, _sz]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -277,6 +278,16 @@ class Crossfader(_Handle):
 
 def bench_uniform(channels, block, ir_len, nblocks, warm, threads, seed=1234) -> float:
     return float(lib().oracle_bench_uniform(channels, block, ir_len, nblocks, warm, threads, seed))
+
+
+BENCH_KINDS = {"uniform": 0, "twostage": 1, "crossfade": 2}
+
+
+def bench(kind, channels, block, ir_len, nblocks, warm, threads, seed=1234, every=0) -> float:
+    """Seconds of `nblocks` process() calls of `block` samples on every one of
+    `channels` instances of `kind` (twostage: block = head block; crossfade:
+    update() with a fresh response every `every` blocks), split over threads."""
+    return float(lib().oracle_bench(BENCH_KINDS[kind], channels, block, ir_len, nblocks, warm, threads, seed, every))
 
 
 def direct_convolution(x, h) -> np.ndarray:

@@ -7,8 +7,16 @@ inputs, HIP events on the launch stream).  Prints one JSON line per config.
   cfg5: CrossfadeConvolver<FFTConvolver>, 512 channels, block 512, IR 96000,
         update() with a fresh IR every 128 blocks (trait init: crossfade over
         response.len() samples, so most updates take the pending path).
+  cfg2u: cfg2 (1024 channels, block 256, IR 48000) with update_device() of
+        every channel every 128 blocks (the post-update launches under
+        rocprofv3 show whether an IR swap costs the process path anything).
 
-Algorithmic bytes per output sample follow SURVEY.md §8(d)."""
+Algorithmic bytes per output sample follow SURVEY.md §8(d).  Each line also
+carries `cpu_baseline` (the oracle port, oracle/fftconv_oracle.c, on a bounded
+sample of the same workload on this host's cores) and, with --pmc, `traffic`:
+per-kernel HBM bytes per launch from separate rocprofv3 --pmc FETCH_SIZE /
+WRITE_SIZE passes of this script (read = 2 x FETCH_SIZE KB, write =
+WRITE_SIZE KB, MI355X_MICROARCH.md's gfx950 correction)."""
 import argparse
 import json
 import os
@@ -70,9 +78,80 @@ def run(conv, C, n_in, n_out, steps, warmup, ring, stream, update=None, batched=
     return max(wall, ev), ev
 
 
+def cpu_baseline(kind, C, block, L, every=0, target_s=6.0):
+    """The oracle port (kind "port": the reference is unbuildable here) timed
+    on this host: one instance per channel, all of this job's threads, a
+    bounded number of blocks (~target_s)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline only
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16, os.cpu_count() or 1))
+    # twostage: whole tail periods (T / head calls) so the tail spike is in the sample
+    warm = 1
+    unit = 1
+    if kind == "twostage":
+        unit = F.compute_tail_block_size(block, L) // block
+        warm = 2 * unit
+    t = oracle.bench(kind, C, block, L, unit, warm, threads, every=every)
+    nb = int(max(unit, min(200000, target_s / max(t / unit, 1e-7))))
+    nb = (nb + unit - 1) // unit * unit
+    if every:
+        nb = max(nb, every)
+    secs = oracle.bench(kind, C, block, L, nb, warm, threads, every=every)
+    return {"value": round(C * block * nb / secs / 1e6, 3), "unit": "MSamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/fftconv_oracle.c {kind}, {C} channels x {nb} blocks of {block} on {threads} threads "
+                      f"in {secs:.1f}s" + (f", update() every {every} blocks" if every else "")}
+
+
+def pmc_kernels(configs, steps_args):
+    """Median HBM bytes per launch of every kernel of this script's run of
+    `configs` (two separate rocprofv3 --pmc passes, before this process
+    touches the GPU).  Returns {kernel name: bytes} or a note string."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return "rocprofv3 not found"
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir="/tmp")
+        cmd = [prof, "--pmc", counter, "--kernel-include-regex", "upols_|ir_segments|la_rebuild", "-d", d, "-o",
+               "pmc", "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--configs", configs,
+               "--no-cpu", "--pmc-inner"] + steps_args
+        try:
+            subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           timeout=300, check=True)
+        except Exception as e:
+            return f"rocprofv3 --pmc {counter} failed: {type(e).__name__}"
+        per = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r.get("Counter_Name") == counter:
+                    per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        for k, v in per.items():
+            vals.setdefault(k, {})[counter] = statistics.median(v)
+    out = {}
+    for k, v in vals.items():
+        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            out[k] = int(2 * v["FETCH_SIZE"] * 1024 + v["WRITE_SIZE"] * 1024)
+    return out
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--configs", default="3,5")
+    p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline legs")
+    p.add_argument("--pmc", action="store_true", help="per-kernel HBM traffic from rocprofv3 --pmc child passes")
+    p.add_argument("--pmc-inner", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--steps2", type=int, default=1024)
     p.add_argument("--steps3", type=int, default=2048)
     p.add_argument("--steps5", type=int, default=512)
     p.add_argument("--sweep", default="",
@@ -81,6 +160,9 @@ def main():
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--variant", type=int, default=-1, help="fftconv_set_kernel_variant for every config")
     a = p.parse_args()
+    traffic = None
+    if a.pmc and not a.pmc_inner:  # (child processes first: this one has not touched the GPU yet)
+        traffic = pmc_kernels(a.configs, ["--steps2", "256", "--steps3", "256", "--steps5", "256"])
     F.set_kernel_variant(a.variant)
     torch.cuda.set_device(0)
     s = torch.cuda.Stream()
@@ -117,6 +199,8 @@ def main():
                         "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
                         "bytes_per_sample": round(per_sample, 1)})
         del conv
+        if not a.no_cpu and not a.pmc_inner:
+            out[-1]["cpu_baseline"] = cpu_baseline("twostage", C, head, L)
     if "5" in a.configs.split(","):
         C, B, L = 512, 512, 96000
         irs = shard.synth_irs(range(C), L)
@@ -145,6 +229,30 @@ def main():
                     "bytes_per_sample": round(per_sample, 1),
                     "canonical_bytes_per_sample": round(2 * uniform_bytes(B, L) / B, 1),
                     "note": "update_device() (HBM-resident IRs: S-segment FFTs per channel) is inside the timed region"})
+        del conv, fresh
+        if not a.no_cpu and not a.pmc_inner:
+            out[-1]["cpu_baseline"] = cpu_baseline("crossfade", C, B, L, every=128)
+    if "2u" in a.configs.split(","):
+        C, B, L = 1024, 256, 48000
+        conv = F.FFTConvolver.init(shard.synth_irs(range(C), L), B, L, channels=C)
+        fresh = [torch.from_numpy(shard.synth_irs(range(2000 + 1000 * j, 2000 + 1000 * j + C), L)).cuda()
+                 for j in range(2)]
+        torch.cuda.synchronize()
+
+        def upd2(i):
+            if i % 128 == 127:
+                conv.update_device(fresh[(i // 128) % 2].data_ptr(), L, L, s.cuda_stream)
+
+        t, ev = run(conv, C, B, B, a.steps2, 200, 32, s, update=upd2)
+        samples = C * B * a.steps2
+        out.append({"config": "cfg2u FFTConvolver, update_device every 128 blocks", "channels": C, "block": B,
+                    "ir": L, "steps": a.steps2, "MSamples_s": round(samples / t / 1e6, 2),
+                    "us_per_step": round(t / a.steps2 * 1e6, 3),
+                    "note": "update_device() (IR transform + window rebuild) inside the timed region"})
+        del conv, fresh
+    if traffic is not None:
+        for o in out:
+            o["traffic_bytes_per_launch"] = traffic
     for o in out:
         print(json.dumps(o), flush=True)
 
