@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -225,6 +226,11 @@ struct UniformCore {
     int la_W = 0;                 // far parts (partial rows per step), 0 = off
     DevPtr<float2> laP, laPm;     // far [C][2][DF][la_W][B] / mid [C][2][DM][B] windows
     unsigned long long la_t = 0;  // lookahead launches so far (stagger clock)
+    // launch timelines of the last `trace_slots` lookahead launches (tuning
+    // only: FFTCONV_LA_TRACE=<slots>, written to FFTCONV_LA_TRACE_OUT at destroy)
+    DevPtr<int4> trace;
+    size_t trace_slots = 0, trace_grid = 0;
+    std::vector<long long> trace_meta;  // per slot: la_t, grid
     int la_seq = 1;               // launch tag, alternating 1 / 2
     bool la_all = true;           // next lookahead launch re-anchors every channel
 
@@ -232,8 +238,27 @@ struct UniformCore {
         if (stream) {
             DeviceGuard g(device);
             (void)order.drain(stream);  // (work still queued on a caller stream reads these buffers)
+            if (trace_slots) dump_trace();
             (void)hipStreamDestroy(stream);
         }
+    }
+
+    void dump_trace() {
+        static int dumps = 0;
+        bool any = false;
+        for (size_t k = 0; k < trace_slots; ++k) any = any || trace_meta[2 * k] >= 0;
+        if (!any) return;
+        std::vector<int4> h(trace.n);
+        if (hipMemcpy(h.data(), trace.p, trace.bytes(), hipMemcpyDeviceToHost) != hipSuccess) return;
+        const char *path = getenv("FFTCONV_LA_TRACE_OUT");
+        const std::string fn = std::string(path ? path : "/tmp/la_trace.bin") + "." + std::to_string(dumps++);
+        FILE *f = fopen(fn.c_str(), "wb");
+        if (!f) return;
+        const long long hdr[4] = {(long long)trace_slots, (long long)trace_grid, (long long)C, (long long)B};
+        fwrite(hdr, sizeof(hdr), 1, f);
+        fwrite(trace_meta.data(), sizeof(long long), trace_meta.size(), f);
+        fwrite(h.data(), sizeof(int4), h.size(), f);
+        fclose(f);
     }
 
     int alloc_geometry(int dev, size_t channels, size_t max_block_size, size_t max_len) {
@@ -262,6 +287,15 @@ struct UniformCore {
             const LaDims d = la_dims(log2b);
             if (int r = laP.alloc(C * 2 * (size_t)d.DF * (size_t)la_W * B)) return r;
             if (int r = laPm.alloc(C * 2 * (size_t)d.DM * B)) return r;
+            if (const char *e = getenv("FFTCONV_LA_TRACE")) {
+                trace_slots = (size_t)std::max(0, atoi(e));
+                trace_grid = (C + 7) / 8 * 8 * (size_t)d.wg_far + C + C + 8;
+                if (trace_slots) {
+                    if (int r = trace.alloc(trace_slots * trace_grid * 8)) return r;
+                    HIP_TRY(hipMemset(trace.p, 0, trace.bytes()));
+                    trace_meta.assign(2 * trace_slots, -1);
+                }
+            }
         }
         // twiddles W_N^k in double, rounded to f32
         std::vector<float2> t(2 * B);
@@ -444,6 +478,14 @@ struct UniformCore {
                 a.mix = *mix;
                 a.mix_tab = mix_tab;
             }
+            if (trace_slots) {
+                const size_t slot = (size_t)(la_t % trace_slots);
+                a.la_trace = trace.p + slot * trace_grid * 8;
+                a.la_trace_grid = (int)trace_grid;
+                trace_meta[2 * slot] = (long long)la_t;
+                trace_meta[2 * slot + 1] = -1;  // (grid: the analysis counts the records)
+                HIP_TRY(hipMemsetAsync(a.la_trace, 0, trace_grid * 8 * sizeof(int4), s));
+            }
             HIP_TRY(launch_process_la(log2b, a, (int)C, s));
             ++la_t;
             la_seq = 3 - la_seq;
@@ -491,6 +533,13 @@ struct UniformCore {
         if (int r = cp(laP, o.laP)) return r;
         if (int r = cp(laPm, o.laPm)) return r;
         la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
+        if (o.trace_slots) {  // (tuning: a clone keeps its own timeline)
+            trace_slots = o.trace_slots;
+            trace_grid = o.trace_grid;
+            if (int r = trace.alloc(trace_slots * trace_grid * 8)) return r;
+            HIP_TRY(hipMemset(trace.p, 0, trace.bytes()));
+            trace_meta.assign(2 * trace_slots, -1);
+        }
         if (int r = staging.alloc(o.staging.n)) return r;
         if (int r = hstage.alloc(o.hstage.n)) return r;
         HIP_TRY(hipStreamSynchronize(stream));

@@ -1352,7 +1352,8 @@ int la_parts(int log2b, int S) {
 }
 LaDims la_dims(int log2b) {
     const int wg = log2b == 7 ? LaGeo<7>::WG_FAR : (log2b == 8 ? LaGeo<8>::WG_FAR : LaGeo<9>::WG_FAR);
-    const bool mid = log2b == 7 ? LaStep<7>::MIDIN : (log2b == 8 ? LaStep<8>::MIDIN : LaStep<9>::MIDIN);
+    static const bool midwg = [] { const char *e = getenv("FFTCONV_LA_MIDWG"); return e && atoi(e) > 0; }();
+    const bool mid = !midwg && (log2b == 7 ? LaStep<7>::MIDIN : (log2b == 8 ? LaStep<8>::MIDIN : LaStep<9>::MIDIN));
     return LaDims{LA_DF, LA_DM, wg, mid ? 1 : 0};
 }
 static int la_probe() {  // timing experiments only: FFTCONV_LA_TIMING_PROBE (results are wrong)

@@ -115,6 +115,10 @@ struct ProcArgs {
     // launch before the next one (la_t = that launch's counter)
     int la_rebuild;
     int la_c0;
+    // launch timeline (tuning only, FFTCONV_LA_TRACE): per wave {role | wave
+    // << 4, HW_ID low 16 bits | XCC_ID << 24, t0, t1} (s_memrealtime, 100 MHz)
+    int4 *la_trace;        // this launch's record: [la_trace_grid][4 waves] + phase stamps after it
+    int la_trace_grid;
 };
 
 struct IrArgs {

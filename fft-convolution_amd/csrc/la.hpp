@@ -52,7 +52,16 @@ constexpr int LA_U = 2;              // anchor: H / X rows in flight per lane
 constexpr int LA_UF = 2;             // far anchor: H / X rows in flight per lane
 constexpr int LA_UM = 2;             // mid anchor: H / X rows in flight per lane
 constexpr int LA_NT = 256;           // threads per workgroup (anchor and step roles)
-constexpr int LA_NG = 4;             // far-row groups
+// LA_HW = 1: far anchors walk their rows in half-wave lanesets (32 lanes = 64
+// bins of a row), 8 far-row groups per workgroup instead of 4 full-wave ones,
+// so each walk is half as long and one workgroup still combines every group
+// in LDS into one window row per step.  Measured (r2g, cfg2, same-process
+// A/B): the far walks end at 12.5 instead of 15.5 us of the launch, but their
+// doubled request rate delays the steps' loads (helpers' pre 11.9 vs 8.7 us)
+// and the launch is slower: 21.60 vs 18.62 us.  The launch is bound by its
+// bytes in flight, not by the far chain alone; kept as an option.
+constexpr int LA_HW = 0;
+constexpr int LA_NG = LA_HW ? 8 : 4; // far-row groups
 constexpr int LA_CU = 8;             // full-pass chain: rows in flight per lane
 constexpr int LA_OOB = 0x7ffffff0;   // a buffer voffset past every stream's range
 static_assert(LA_DM <= LA_D1 && LA_DM <= 8 && LA_DF <= 32 && LA_DF % LA_JW == 0, "lookahead levels (state word fields)");
@@ -120,6 +129,10 @@ __device__ __forceinline__ int la_dnew(int c, const ProcArgs &a, int P) {
 // would meet blocks not yet written) and stores only the steps it owns
 __host__ __device__ constexpr int la_mid_per(int L) { return (LA_DM + (L < LA_DM ? L : LA_DM) - 1) / (L < LA_DM ? L : LA_DM); }
 __device__ __forceinline__ int la_mid_j0(int l, int JM) { return min(l * JM, LA_DM - JM); }
+// far-row group g walks descending (LA_HW: every group, so the two groups of a
+// wave share their walk direction) or ascending for odd g (full-wave groups:
+// neighbouring groups then read their shared X rows at the same time)
+__host__ __device__ constexpr bool la_asc(int g) { return LA_HW ? false : (g & 1) != 0; }
 // far-row group g of NG: rows [lo, hi) of [DF+1, act)
 __device__ __forceinline__ void la_group(int g, int act, int &lo, int &hi) {
     const int nf = act - LA_DF - 1;
@@ -194,6 +207,48 @@ __device__ __forceinline__ void la_walk(LaAcc (&acc)[JW], const RowStream &hs, c
     }
 }
 
+// The far walk of a half-wave laneset (LA_HW): rows [lo, hi) descending, with
+// lo / hi per lane (a wave holds two lanesets, i.e. two far-row groups), so
+// every offset is a per-lane voffset; `nmax` = the wave's longer walk, the
+// shorter one idles its last row.  Same accumulator order as la_walk
+// (descending): acc[jj] += H[i] (.) X(age i - j0 - 1 - jj at the anchor).
+template <int LOG2B, int JW, int U>
+__device__ __forceinline__ void la_walk_lane(LaAcc (&acc)[JW], const RowStream &hs, const RowStream &xs, int voff,
+                                             bool z0, int lo, int hi, int nmax, int j0, int cur, int act) {
+    constexpr int ROWB = (1 << LOG2B) * (int)sizeof(float2);
+    constexpr int RS = JW + U;
+    constexpr int UNR = RS % U == 0 ? RS : RS * U;
+    const int n = hi - lo;
+    const int ne = n + JW - 1;
+    auto xo = [&](int e) {  // X ring entry e: age hi - 2 - j0 - e >= 1
+        int r = cur + hi - 2 - j0 - e;
+        if (r >= act) r -= act;
+        return e < ne ? voff + r * ROWB : LA_OOB;
+    };
+    auto ho = [&](int k) { return k < n ? voff + (hi - 1 - k) * ROWB : LA_OOB; };
+    float4 xr[RS], hr[U];
+#pragma unroll
+    for (int e = 0; e < RS - 1; ++e) xr[e] = xs.ld4<false>(xo(e), 0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) hr[k] = hs.ld4<false>(ho(k), 0);
+#pragma nounroll
+    for (int k0 = 0; k0 < nmax; k0 += UNR) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const int k = k0 + u;
+            if (k >= nmax) break;
+            if (k < n) {
+                const LaH h = la_ops(hr[u % U], z0);
+#pragma unroll
+                for (int jj = 0; jj < JW; ++jj) acc[jj].mac(h, xr[(u + jj) % RS]);
+            }
+            hr[u % U] = hs.ld4<false>(ho(k + U), 0);
+            xr[(u + RS - 1) % RS] = xs.ld4<false>(xo(k + RS - 1), 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 // One chain for the current step (X age i), the same rows in the same order
 // as an anchor's accumulators.
 template <int LOG2B, bool ASC, bool NTL>
@@ -226,7 +281,8 @@ struct LaGeo {
     // GPW far groups (one wave-sized laneset each) of one window slice of JW
     // steps, combined in LDS; one anchor = NSL slices x WF parts x (DF / JW)
     // window slices, XCD-aligned (see la_anchor_far)
-    static constexpr int FS = F < 64 ? F : 64, NSL = F / FS, LPF = LA_NT / FS;
+    static constexpr int FW = LA_HW ? 32 : 64;                      // lanes per far laneset
+    static constexpr int FS = F < FW ? F : FW, NSL = F / FS, LPF = LA_NT / FS;
     static constexpr int GPW = LPF < LA_NG ? LPF : LA_NG;
     static constexpr int WF = LA_NG / GPW;                          // far parts (P rows per step)
     static_assert(LA_NG % GPW == 0, "far groups must fill whole parts");
@@ -311,8 +367,9 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
 
     constexpr int FS = LG::FS, NSL = LG::NSL;
     const int tid = threadIdx.x;
-    const int l = __builtin_amdgcn_readfirstlane(tid / FS), fl = tid % FS;
-    if (l >= GPW) return;                              // (more lanesets than groups)
+    // (LA_HW: a laneset is half a wave, its index is per lane)
+    const int l = LA_HW ? tid / FS : __builtin_amdgcn_readfirstlane(tid / FS), fl = tid % FS;
+    if (!LA_HW && l >= GPW) return;                    // (more lanesets than groups)
     const int f = (r % NSL) * FS + fl;                 // bin slice
     const int w = (r / NSL) % LG::WF;                  // part
     const int h = r / (NSL * LG::WF);                  // window slice: steps h*JW+1 .. h*JW+JW
@@ -327,8 +384,16 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
     for (int j = 0; j < LA_JW; ++j) acc[j].zero();
     // (plain loads: the nontemporal policy streamed no faster here and cost the
     // step workgroups' cache-resident near rows ~8 % of the launch, r1i_la15_ab)
-    if (hi > lo) {
-        if (g & 1) la_walk<LOG2B, true, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+    if constexpr (LA_HW) {
+        static_assert(LG::FS * 2 == 64 && LG::WF == 1, "half-wave far lanesets");
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+        int lo0, hi0, lo1, hi1;  // the wave's two groups
+        la_group(2 * wv, act, lo0, hi0);
+        la_group(2 * wv + 1, act, lo1, hi1);
+        const int nmax = max(hi0 - lo0, hi1 - lo1);
+        if (nmax > 0) la_walk_lane<LOG2B, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, nmax, h * LA_JW, cur, act);
+    } else if (hi > lo) {
+        if (la_asc(g)) la_walk<LOG2B, true, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
         else la_walk<LOG2B, false, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
     }
     if constexpr (GPW > 1) {
@@ -411,6 +476,14 @@ struct LaStep {
     static constexpr size_t bytes = chain_bytes > grp_bytes ? chain_bytes : grp_bytes;
 };
 
+// launch timeline phase stamp k (0..3) of this wave (FFTCONV_LA_TRACE)
+__device__ __forceinline__ void la_stamp(const ProcArgs &a, int k) {
+    if (a.la_trace && (threadIdx.x & 63) == 0) {
+        int *p = reinterpret_cast<int *>(a.la_trace + ((size_t)a.la_trace_grid * 4 + (size_t)blockIdx.x * 4 + (threadIdx.x >> 6)));
+        p[k] = (int)(unsigned)__builtin_amdgcn_s_memrealtime();
+    }
+}
+
 template <int LOG2B, bool NTL, int NCH, int XF>
 __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, const int (&cs)[NCH],
                                         const int4 (&st)[NCH], int nvalid, unsigned char *smem) {
@@ -472,7 +545,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 }
                 LaAcc acc;
                 acc.zero();
-                if (q > 0 && ((q - 1) & 1)) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+                if (q > 0 && la_asc(q - 1)) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
                 else la_chain<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
                 grp[(k * NCHAIN + q) * F + f] = acc.get();
             }
@@ -530,6 +603,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             dma_f32<64>(p1l, a.mix_tab, B);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        la_stamp(a, 0);
         if constexpr (NCH > 1) {
             __syncthreads();  // wave 0's twiddle table is in LDS
         } else {
@@ -549,6 +623,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             Q[m] = v;
             Xcur[m] = v;
         }
+        la_stamp(a, 1);
     } else {
         if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
         // ---- pre = near chain (rows D1..1) + (mid + far), canonical order
@@ -588,11 +663,14 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             float2 *prel = reinterpret_cast<float2 *>(chan_lds(k)) + 3 * B;
             reinterpret_cast<float4 *>(prel)[f] = vadd(acc.get(), vadd(M, A));
         }
+        la_stamp(a, 0);
     }
     __syncthreads();
+    la_stamp(a, 2);
     if (wave >= NCH) {
         if (a.la_probe >= 5) return;  // (timing probes 5/6: steps without their mid anchors)
         if constexpr (LS::MIDIN) {
+          if (a.la_nmid == 0) {  // (FFTCONV_LA_MIDWG: mid anchors in workgroups of their own)
             // mid anchors of this workgroup's scheduled channels: rows DF..D1+1
             // for the next DM steps (the pre-launch ring position is at hand)
             constexpr int LH = HL / F;                    // helper lanesets
@@ -620,6 +698,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                         if (j0 + j >= l * JMS && j0 + j < d) la_pm(a, c, win, j0 + j, B)[f] = acc[j].get();
                 }
             }
+          }
         }
         return;
     }
@@ -637,6 +716,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     float *ovc = J.overlap + c * B;
     // crossfade, B's launch: out = mix(A's block, this block) (:75-77)
     bool bad = false;  // conv = pre + X (.) H[0] (:256-261), then the C2R error check
+    la_stamp(a, 3);
     for (int f = lane; f < F; f += 64) {
         const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
                                    reinterpret_cast<const float4 *>(h0l)[f], f);
@@ -763,10 +843,9 @@ __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsign
 // whose first workgroup also writes the gains of this call's mix_value walk to mix_tab;
 // 2 = B's launch, whose steps mix A's block with their own
 template <int LOG2B, bool NTL, int XF>
-__global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
+__device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char *smem) {
     using LS = LaStep<LOG2B>;
     constexpr int NCH = LS::NCH;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if constexpr (XF == 1) {
         // 8 extra workgroups at the front of the grid (one per XCD: the far
         // anchors' XCD placement behind them is unchanged); the first walks,
@@ -810,4 +889,34 @@ __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
         la_step<LOG2B, NTL, NCH, XF>(a, J, cs, st, nvalid, smem);
     else  // (the arguments by their kernarg address: no private copy of the block)
         la_fallback<LOG2B, NTL, XF>((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), c0, nvalid, smem);
+}
+
+// the role of workgroup blockIdx.x in a lookahead launch (for the timeline)
+template <int XF>
+__device__ __forceinline__ int la_role(const ProcArgs &a) {
+    if (XF == 1 && blockIdx.x < LA_XWG) return 4;  // mix walk
+    const int nanchor = a.la_nfar + a.la_nmid;
+    const int nstep = (int)gridDim.x - nanchor - (XF == 1 ? LA_XWG : 0);
+    const int b = (int)blockIdx.x - (XF == 1 ? LA_XWG : 0);
+    const int ba = a.la_steps_first ? b - nstep : b;
+    if (ba >= 0 && ba < nanchor) return ba < a.la_nfar ? 0 : 1;  // far / mid anchor
+    return 2;                                                       // step
+}
+
+template <int LOG2B, bool NTL, int XF>
+__global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned t0 = 0;
+    if (a.la_trace) t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+    la_kernel_body<LOG2B, NTL, XF>(a, smem);
+    if (a.la_trace) {
+        const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
+        const int wave = (int)(threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0) {
+            const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID
+            const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+            a.la_trace[(size_t)blockIdx.x * 4 + wave] =
+                make_int4(la_role<XF>(a) | (wave << 4), (int)((hw & 0xffffu) | ((xcc & 0xffu) << 24)), (int)t0, (int)t1);
+        }
+    }
 }
