@@ -16,7 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -445,6 +447,42 @@ struct UniformCore {
         return j;
     }
 
+    // a full-block call takes the lookahead launch
+    bool la_ready(size_t n) const { return la_W && n == B && la_parts(log2b, (int)S) == la_W; }
+
+    // this batch's lookahead fields of a launch: windows, stagger clock,
+    // anchor workgroup counts (and the timeline record, when tracing)
+    int la_fill(ProcArgs &a, hipStream_t s) {
+        const LaDims d = la_dims(log2b);
+        auto count = [&](size_t P) {
+            const size_t t0 = (size_t)(la_t % P);
+            return la_all ? C : (C > t0 ? (C - t0 + P - 1) / P : 0);
+        };
+        a.laP = laP.p;
+        a.laPm = laPm.p;
+        a.la_W = la_W;
+        a.la_all = la_all ? 1 : 0;
+        a.la_t = (int)(la_t % (unsigned long long)(d.DF * d.DM));  // (both periods divide it)
+        a.la_seq = la_seq;
+        // (far anchors: whole rounds of 8 channels, one XCD each -- see la_anchor_far)
+        a.la_nfar = (int)((count((size_t)d.DF) + 7) / 8 * 8 * (size_t)d.wg_far);
+        a.la_nmid = d.mid_in_step ? 0 : (int)count((size_t)d.DM);
+        if (trace_slots) {
+            const size_t slot = (size_t)(la_t % trace_slots);
+            a.la_trace = trace.p + slot * trace_grid * 8;
+            a.la_trace_grid = (int)trace_grid;
+            trace_meta[2 * slot] = (long long)la_t;
+            trace_meta[2 * slot + 1] = -1;  // (grid: the analysis counts the records)
+            HIP_TRY(hipMemsetAsync(a.la_trace, 0, trace_grid * 8 * sizeof(int4), s));
+        }
+        return FFTCONV_OK;
+    }
+    void la_advance() {
+        ++la_t;
+        la_seq = 3 - la_seq;
+        la_all = false;
+    }
+
     // la_mix / mix / mix_tab: crossfade fusion on the lookahead step (ProcArgs::la_mix);
     // the caller only passes them when this call takes the lookahead launch
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t n, hipStream_t s,
@@ -455,41 +493,18 @@ struct UniformCore {
         a.job[0] = job(din, is, dout, os, n);
         a.tw = tw.p;
         a.njobs = 1;
-        if (la_W && n == B && la_parts(log2b, (int)S) == la_W) {
+        if (la_ready(n)) {
             // lookahead launch: the step workgroups behind this launch's far
             // and mid anchors (every channel on entry, else the stagger
             // classes (c - t) % period == 0)
-            const LaDims d = la_dims(log2b);
-            auto count = [&](size_t P) {
-                const size_t t0 = (size_t)(la_t % P);
-                return la_all ? C : (C > t0 ? (C - t0 + P - 1) / P : 0);
-            };
-            a.laP = laP.p;
-            a.laPm = laPm.p;
-            a.la_W = la_W;
-            a.la_all = la_all ? 1 : 0;
-            a.la_t = (int)(la_t % (unsigned long long)(d.DF * d.DM));  // (both periods divide it)
-            a.la_seq = la_seq;
-            // (far anchors: whole rounds of 8 channels, one XCD each -- see la_anchor_far)
-            a.la_nfar = (int)((count((size_t)d.DF) + 7) / 8 * 8 * (size_t)d.wg_far);
-            a.la_nmid = d.mid_in_step ? 0 : (int)count((size_t)d.DM);
+            if (int r = la_fill(a, s)) return r;
             if (la_mix && mix) {
                 a.la_mix = la_mix;
                 a.mix = *mix;
                 a.mix_tab = mix_tab;
             }
-            if (trace_slots) {
-                const size_t slot = (size_t)(la_t % trace_slots);
-                a.la_trace = trace.p + slot * trace_grid * 8;
-                a.la_trace_grid = (int)trace_grid;
-                trace_meta[2 * slot] = (long long)la_t;
-                trace_meta[2 * slot + 1] = -1;  // (grid: the analysis counts the records)
-                HIP_TRY(hipMemsetAsync(a.la_trace, 0, trace_grid * 8 * sizeof(int4), s));
-            }
             HIP_TRY(launch_process_la(log2b, a, (int)C, s));
-            ++la_t;
-            la_seq = 3 - la_seq;
-            la_all = false;
+            la_advance();
             return FFTCONV_OK;
         }
         if (la_W) la_all = true;  // this launch drops every window
@@ -543,6 +558,25 @@ struct UniformCore {
         if (int r = staging.alloc(o.staging.n)) return r;
         if (int r = hstage.alloc(o.hstage.n)) return r;
         HIP_TRY(hipStreamSynchronize(stream));
+        return FFTCONV_OK;
+    }
+
+    // segments_ir[seg] of channel c as the reference holds it: B+1 bins,
+    // interleaved (re, im), unpacked from the (DC, Nyquist) slot
+    int ir_spectrum(size_t c, size_t seg, float *out) {
+        if (c >= C || seg >= S) return fail(FFTCONV_E_INVALID, "channel or segment out of range");
+        DeviceGuard g(device);
+        if (int r = order.drain(stream)) return r;
+        std::vector<float2> row(B);
+        HIP_TRY(hipMemcpy(row.data(), H.p + (c * S + seg) * B, B * sizeof(float2), hipMemcpyDeviceToHost));
+        out[0] = row[0].x;
+        out[1] = 0.f;
+        for (size_t k = 1; k < B; ++k) {
+            out[2 * k] = row[k].x;
+            out[2 * k + 1] = row[k].y;
+        }
+        out[2 * B] = row[0].y;
+        out[2 * B + 1] = 0.f;
         return FFTCONV_OK;
     }
 
@@ -1075,6 +1109,29 @@ struct CrossfadeCore {
             // :72-73 on the lookahead step: each convolver's full
             // block runs its own launch of far / mid anchors and steps; then
             // the mix (:75-77)
+            static const bool split = [] { const char *e = getenv("FFTCONV_XF_SPLIT"); return e && atoi(e) > 0; }();
+            if (out_len == m && la_fuse_mix_allowed() && !split && a->la_t == b->la_t && a->la_seq == b->la_seq &&
+                a->la_all == b->la_all) {
+                // :72-77 in ONE launch: A's and B's anchors, and per channel
+                // one workgroup running A's and B's step (two chain waves)
+                // that mixes the two blocks in LDS -- A's and B's clocks
+                // agree (they step together), so one stagger serves both
+                ProcArgs pa{};
+                pa.job[0] = a->job(din, is, dout, os, m);
+                pa.job[1] = b->job(din, is, nullptr, 0, m);
+                pa.tw = a->tw.p;
+                pa.njobs = 2;
+                if (int r = a->la_fill(pa, s)) return r;
+                pa.laP2 = b->laP.p;
+                pa.laPm2 = b->laPm.p;
+                pa.la_mix = 3;
+                pa.mix = mix_args(dout, os, out_len);  // (buf_a / buf_b: the generic-step fallback)
+                HIP_TRY(launch_process_la(a->log2b, pa, (int)C, s));
+                a->la_advance();
+                b->la_advance();
+                xf.advance(out_len);
+                return FFTCONV_OK;
+            }
             if (out_len == m && la_fuse_mix_allowed()) {
                 // the mix fused into B's launch: A's launch walks mix_value
                 // once into mix_tab, B's epilogue mixes A's block (buf_a) with
@@ -1165,6 +1222,74 @@ struct CrossfadeCore {
     }
 };
 
+// W_N^k tables of the stand-alone Fft entry points, one per (device, N),
+// built on first use in f64 and kept for the process (the handles keep
+// their own); the same values as every handle's table for that N.
+int fft_twiddles(int dev, int log2n, const float2 **out) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, float2 *> tabs;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = tabs.find({dev, log2n});
+    if (it != tabs.end()) {
+        *out = it->second;
+        return FFTCONV_OK;
+    }
+    const size_t N = (size_t)1 << log2n;
+    std::vector<float2> t(N);
+    for (size_t k = 0; k < N; ++k) {
+        const double ang = -2.0 * M_PI * (double)k / (double)N;
+        t[k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+    }
+    float2 *p = nullptr;
+    HIP_TRY(hipMalloc((void **)&p, N * sizeof(float2)));
+    HIP_TRY(hipMemcpy(p, t.data(), N * sizeof(float2), hipMemcpyHostToDevice));
+    tabs[{dev, log2n}] = p;
+    *out = p;
+    return FFTCONV_OK;
+}
+
+// Fft::forward / inverse on device rows (src/fft_convolver.rs:36-49)
+int fft_rows(int device, size_t n, size_t rows, const float *din, size_t is, float *dout, size_t os, int *status,
+             bool inverse, hipStream_t s) {
+    if (int r = check_device(device)) return r;
+    if (n < 2 || (n & (n - 1)) || n > ((size_t)2 << kMaxLog2Block))
+        return fail(FFTCONV_E_UNSUPPORTED, "Fft length must be a power of two in 2..16384 (N = 2 * block)");
+    const size_t cin = inverse ? n + 2 : n, cout = inverse ? n : n + 2;
+    if (rows > (size_t)INT32_MAX || (rows > 1 && (is < cin || os < cout)))
+        return fail(FFTCONV_E_INVALID, "row strides shorter than a row");
+    if (rows == 0) return FFTCONV_OK;
+    DeviceGuard g(device);
+    const float2 *tw = nullptr;
+    if (int r = fft_twiddles(device, ilog2(n), &tw)) return r;
+    FftArgs a{};
+    a.in = din; a.in_stride = (long long)is; a.out = dout; a.out_stride = (long long)os; a.tw = tw; a.status = status;
+    HIP_TRY(launch_fft_rows(ilog2(n) - 1, inverse, a, (int)rows, s));
+    return FFTCONV_OK;
+}
+
+// host-memory form: rows packed ([rows][n] reals, [rows][n + 2] bin floats),
+// through temporary device buffers on a private stream; synchronous
+int fft_rows_host(int device, size_t n, size_t rows, const float *in, float *out, int *status, bool inverse) {
+    if (int r = check_device(device)) return r;
+    if (rows == 0) return FFTCONV_OK;
+    DeviceGuard g(device);
+    const size_t cin = inverse ? n + 2 : n, cout = inverse ? n : n + 2;
+    DevPtr<float> din, dout;
+    DevPtr<int> dst;
+    if (int r = din.alloc(rows * cin)) return r;
+    if (int r = dout.alloc(rows * cout)) return r;
+    if (status) { if (int r = dst.alloc(rows)) return r; }
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    struct Del { hipStream_t s; ~Del() { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); } } del{s};
+    HIP_TRY(hipMemcpyAsync(din.p, in, rows * cin * sizeof(float), hipMemcpyHostToDevice, s));
+    if (int r = fft_rows(device, n, rows, din.p, cin, dout.p, cout, status ? dst.p : nullptr, inverse, s)) return r;
+    HIP_TRY(hipMemcpyAsync(out, dout.p, rows * cout * sizeof(float), hipMemcpyDeviceToHost, s));
+    if (status) HIP_TRY(hipMemcpyAsync(status, dst.p, rows * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFTCONV_OK;
+}
+
 template <class T>
 T *make_or_null(int r, T *p) {
     if (r != FFTCONV_OK) {
@@ -1195,6 +1320,22 @@ int fftconv_device_count(void) {
     return n;
 }
 size_t fftconv_complex_size(size_t size) { return size / 2 + 1; }
+
+// ---- Fft (src/fft_convolver.rs:7-50) ---------------------------------------
+int fftconv_fft_forward(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
+                        size_t out_stride, void *hip_stream) {
+    return fft_rows(device, n, rows, d_in, in_stride, d_out, out_stride, nullptr, false, (hipStream_t)hip_stream);
+}
+int fftconv_fft_inverse(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
+                        size_t out_stride, int *d_status, void *hip_stream) {
+    return fft_rows(device, n, rows, d_in, in_stride, d_out, out_stride, d_status, true, (hipStream_t)hip_stream);
+}
+int fftconv_fft_forward_host(int device, size_t n, size_t rows, const float *input, float *output) {
+    return fft_rows_host(device, n, rows, input, output, nullptr, false);
+}
+int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *input, float *output, int *status) {
+    return fft_rows_host(device, n, rows, input, output, status, true);
+}
 
 // compute_tail_block_size, src/fft_convolver.rs:514-526, in f32 exactly as written
 size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
@@ -1317,6 +1458,10 @@ size_t fftconv_uniform_channels(const fftconv_uniform *h) { return h ? h->core.C
 int fftconv_uniform_lookahead_parts(const fftconv_uniform *h) { return h ? h->core.la_W : 0; }
 size_t fftconv_uniform_block_size(const fftconv_uniform *h) { return h ? h->core.B : 0; }
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h) { return h ? h->core.S : 0; }
+int fftconv_uniform_ir_spectrum(const fftconv_uniform *h, size_t channel, size_t segment, float *out) {
+    if (!h) return fail(FFTCONV_E_INVALID, "null handle");
+    return const_cast<UniformCore &>(h->core).ir_spectrum(channel, segment, out);
+}
 int fftconv_uniform_channel_state(const fftconv_uniform *h, size_t channel, size_t out3[3]) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     return const_cast<UniformCore &>(h->core).channel_state(channel, out3);

@@ -1180,6 +1180,67 @@ __global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Fft::forward / Fft::inverse as a batched API (src/fft_convolver.rs:36-49):
+// realfft's even-length algorithm, the same butterflies and twiddles as the
+// convolver's transforms, so an IR segment's spectrum here is bit-identical
+// to the row the convolver holds for it.  Forward: N reals -> M+1 bins,
+// unnormalised, DC / Nyquist imaginary parts exactly 0.  Inverse: M+1 bins ->
+// N reals divided by N (:44-46); a non-zero DC / Nyquist imaginary part is
+// realfft's FftError::InputValues -- flagged in status, and (like the oracle's
+// restatement) the transform runs with those parts taken as 0.
+// ---------------------------------------------------------------------------
+template <int LOG2M, int NT, bool INV>
+__global__ __launch_bounds__(NT) void fft_rows_kernel(FftArgs a) {
+    constexpr int M = 1 << LOG2M;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *bufA = reinterpret_cast<float2 *>(smem);
+    float2 *bufB = bufA + M;
+    const int tid = threadIdx.x;
+    const float *in = a.in + (size_t)blockIdx.x * a.in_stride;
+    float *out = a.out + (size_t)blockIdx.x * a.out_stride;
+    if constexpr (!INV) {
+        for (int m = tid; m < M; m += NT) bufA[m] = make_float2(in[2 * m], in[2 * m + 1]);
+        __syncthreads();
+        const float2 *Z = lds_cfft<LOG2M, NT, false>(bufA, bufB, a.tw);
+        for (int k = tid; k < M; k += NT) {
+            const float2 v = real_post<LOG2M, NT>(Z, k, a.tw);
+            if (k == 0) {  // packed (DC, Nyquist)
+                out[0] = v.x;
+                out[1] = 0.f;
+                out[2 * M] = v.y;
+                out[2 * M + 1] = 0.f;
+            } else {
+                out[2 * k] = v.x;
+                out[2 * k + 1] = v.y;
+            }
+        }
+    } else {
+        constexpr float invN = 1.0f / (float)(2 * M);
+        for (int k = tid; k < M; k += NT)
+            bufA[k] = k == 0 ? make_float2(in[0], in[2 * M]) : make_float2(in[2 * k], in[2 * k + 1]);
+        if (tid == 0 && a.status) a.status[blockIdx.x] = (in[1] != 0.f || in[2 * M + 1] != 0.f) ? 1 : 0;
+        __syncthreads();
+        for (int m = tid; m < M; m += NT) bufB[m] = real_pre<LOG2M, NT>(bufA, m, a.tw);
+        __syncthreads();
+        const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2M, NT, true>(bufB, bufA, a.tw));
+        for (int j = tid; j < 2 * M; j += NT) out[j] = y[j] * invN;  // (x / N: N is a power of two)
+    }
+}
+
+template <int LOG2M>
+static hipError_t launch_fft_t(bool inverse, const FftArgs &a, int rows, hipStream_t s) {
+    constexpr int NT = LOG2M <= 6 ? 64 : 256;
+    constexpr size_t lds = 2 * (size_t)(1 << LOG2M) * sizeof(float2) + 16;
+    auto kern = inverse ? fft_rows_kernel<LOG2M, NT, true> : fft_rows_kernel<LOG2M, NT, false>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(rows), dim3(NT), lds, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // TwoStage sub-chunk (src/fft_convolver.rs:438-461): output += precalculated0
 // then += precalculated (two passes, like the reference), and append the
 // input to tail_input.
@@ -1360,6 +1421,10 @@ static int la_probe() {  // timing experiments only: FFTCONV_LA_TIMING_PROBE (re
     static const int v = [] { const char *e = getenv("FFTCONV_LA_TIMING_PROBE"); return e ? atoi(e) : 0; }();
     return v;
 }
+static int xf_steps_first() {  // crossfade (la_mix 3) grid order, FFTCONV_XF_STEPS_FIRST (tuning)
+    static const int v = [] { const char *e = getenv("FFTCONV_XF_STEPS_FIRST"); return e ? atoi(e) : 1; }();
+    return v;
+}
 static int la_steps_first() {
     static const int v = [] { const char *e = getenv("FFTCONV_LA_STEPS_FIRST"); return e ? atoi(e) : 0; }();
     return v;
@@ -1371,25 +1436,31 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         return hipErrorNotSupported;
     } else {
         using LG = LaGeo<LOG2B>;
-        using LS = LaStep<LOG2B>;
+        const bool xf3 = a.la_mix == 3;
+        const size_t lsb = xf3 ? LaStep<LOG2B, 3>::bytes : LaStep<LOG2B>::bytes;
+        const int nch = xf3 ? 1 : LaStep<LOG2B>::NCH;  // channels per step workgroup
         constexpr size_t gen = Geo<LOG2B, LA_NT>::lds_bytes;
-        constexpr size_t lds0 = LS::bytes > LG::anchor_bytes ? LS::bytes : LG::anchor_bytes;
-        constexpr size_t lds1 = lds0 > gen ? lds0 : gen;
-        constexpr size_t lds = (lds1 + 15) / 16 * 16;
+        const size_t lds0 = lsb > LG::anchor_bytes ? lsb : LG::anchor_bytes;
+        const size_t lds1 = lds0 > gen ? lds0 : gen;
+        const size_t lds = (lds1 + 15) / 16 * 16;
         if (a.la_W != LG::WF || !a.laPm) return hipErrorInvalidValue;
+        if (xf3 && (a.njobs != 2 || !a.laP2 || !a.laPm2 || a.job[0].S != a.job[1].S || a.job[0].n != a.job[1].n ||
+                    a.job[0].add0 || a.job[1].add0 || !a.mix.buf_a || !a.mix.buf_b))
+            return hipErrorInvalidValue;
         // the far-row streams: nontemporal once the whole H + FDL working set
         // (re-read every D steps) exceeds the Infinity Cache
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
         const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
         auto kern = a.la_mix == 1   ? (ntl ? upols_la_kernel<LOG2B, true, 1> : upols_la_kernel<LOG2B, false, 1>)
                     : a.la_mix == 2 ? (ntl ? upols_la_kernel<LOG2B, true, 2> : upols_la_kernel<LOG2B, false, 2>)
+                    : xf3           ? (ntl ? upols_la_kernel<LOG2B, true, 3> : upols_la_kernel<LOG2B, false, 3>)
                                     : (ntl ? upols_la_kernel<LOG2B, true, 0> : upols_la_kernel<LOG2B, false, 0>);
         ProcArgs args = a;
         args.pipe = 0;
         args.lag = 0;
         args.la_channels = channels;
-        args.la_steps_first = la_steps_first();
-        args.la_probe = la_probe();
+        args.la_steps_first = xf3 ? xf_steps_first() : la_steps_first();
+        args.la_probe = xf3 ? 0 : la_probe();
         if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) {
             args.la_all = -1;  // no anchors: every eligible step sums all its rows
             args.la_nfar = args.la_nmid = 0;
@@ -1398,17 +1469,18 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
-        const int nstep = (channels + LS::NCH - 1) / LS::NCH;
+        const int nstep = (channels + nch - 1) / nch;
         if (a.la_mix == 2 && a.job[0].add0) return hipErrorInvalidValue;  // (the fused mix uses the add buffers' LDS)
         const int xwg = a.la_mix == 1 ? LA_XWG : 0;  // A's launch: the mix_value walk workgroups
-        hipLaunchKernelGGL(kern, dim3(args.la_nfar + args.la_nmid + nstep + xwg), dim3(LA_NT), lds, s, args);
+        const int nanch = (xf3 ? 2 : 1) * (args.la_nfar + args.la_nmid);
+        hipLaunchKernelGGL(kern, dim3(nanch + nstep + xwg), dim3(LA_NT), lds, s, args);
         return hipGetLastError();
     }
 }
 
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;
-    if (a.njobs != 1 || !a.laP) return hipErrorInvalidValue;
+    if (a.njobs != (a.la_mix == 3 ? 2 : 1) || !a.laP) return hipErrorInvalidValue;
     FFTCONV_DISPATCH(launch_la_t, log2b, a, channels, s)
 }
 
@@ -1425,8 +1497,8 @@ template <int LOG2B, bool NTL>
 __global__ __launch_bounds__(LA_NT, 4) void la_rebuild_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int b = (int)blockIdx.x;
-    if (b < a.la_nfar) la_anchor_far<LOG2B, NTL>(a, b, smem);
-    else la_anchor_mid<LOG2B, NTL>(a, b - a.la_nfar);
+    if (b < a.la_nfar) la_anchor_far<LOG2B, NTL>(a, 0, b, smem);
+    else la_anchor_mid<LOG2B, NTL>(a, 0, b - a.la_nfar);
 }
 
 // the state words of the rebuilt windows (same eligibility test as the
@@ -1487,6 +1559,11 @@ bool la_full_variant() { return g_variant != VARIANT_AUTO && (g_variant & VARIAN
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s) {
     if (channels <= 0 || a.S <= 0) return hipSuccess;
     FFTCONV_DISPATCH(launch_ir_t, log2b, a, channels, s)
+}
+
+hipError_t launch_fft_rows(int log2m, bool inverse, const FftArgs &a, int rows, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    FFTCONV_DISPATCH(launch_fft_t, log2m, inverse, a, rows, s)
 }
 
 hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipStream_t s) {

@@ -24,7 +24,11 @@ enum : int {
     LA_JM_SHIFT = 18,
     LA_DM_SHIFT = 21,
     SEQ_SHIFT = 24,
-    LA_MASK = FLAG_LA | FLAG_LAM | (31 << LA_J_SHIFT) | (31 << LA_D_SHIFT) | (7 << LA_JM_SHIFT) | (7 << LA_DM_SHIFT),
+    // lookahead: pre[] holds the near rows' sum (rows D1..1) of the block
+    // that starts at `current`, left by the previous step (la.hpp)
+    FLAG_NEAR = 1 << 26,
+    LA_MASK = FLAG_LA | FLAG_LAM | (31 << LA_J_SHIFT) | (31 << LA_D_SHIFT) | (7 << LA_JM_SHIFT) | (7 << LA_DM_SHIFT) |
+              FLAG_NEAR,
     SEQ_MASK = 3 << SEQ_SHIFT,
 };
 
@@ -95,6 +99,7 @@ struct ProcArgs {
     // lookahead launch (launch_process_la; job[0] only)
     float2 *laP;           // [C][2 windows][LA_DF][la_W][B] far-row partial sums
     float2 *laPm;          // [C][2 windows][LA_DM][B] mid-row partial sums
+    float2 *laP2, *laPm2;  // job[1]'s windows (la_mix 3: the crossfade's B in the same launch)
     int la_W;              // far parts (partial rows per step)
     int la_nfar;           // far anchor workgroups at the front of the grid
     int la_nmid;           // mid anchor workgroups after them
@@ -107,7 +112,9 @@ struct ProcArgs {
     int la_channels;       // channels of the batch (step workgroups cover LaStep::NCH each)
     // crossfade on the lookahead step (CrossfadeConvolver::process :72-77):
     // 1 = A's launch also writes this call's per-sample mix selectors to mix_tab;
-    // 2 = B's launch mixes in its epilogue: out = mix(mix.buf_a, B's block)
+    // 2 = B's launch mixes in its epilogue: out = mix(mix.buf_a, B's block);
+    // 3 = ONE launch for A (job[0]) and B (job[1]): a step workgroup runs A's
+    //     and B's chain of one channel and mixes in LDS (out = job[0].out)
     int la_mix;
     float *mix_tab;        // [n] mix_selector of each sample (la_mix 1 writes, 2 reads)
     // window rebuild (launch_la_rebuild, after update / reset / init): anchors
@@ -151,6 +158,20 @@ struct TwoStageAccumArgs {
     int cnt;               // samples in the sub-chunk
 };
 
+
+// Fft::forward / Fft::inverse (src/fft_convolver.rs:36-49) over rows of
+// N = 2M reals / M+1 interleaved complex bins (the public Fft of the
+// reference, fftconv_fft_*): one workgroup per row, the convolver's own
+// transforms (lds_cfft + real_post / real_pre, the same twiddle table)
+struct FftArgs {
+    const float *in;
+    long long in_stride;   // floats between rows
+    float *out;
+    long long out_stride;
+    const float2 *tw;      // W_N^k, k < N
+    int *status;           // inverse: per row 1 = FftError::InputValues (DC / Nyquist imag != 0), or null
+};
+hipError_t launch_fft_rows(int log2m, bool inverse, const FftArgs &a, int rows, hipStream_t s);
 
 hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s);

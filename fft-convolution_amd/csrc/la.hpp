@@ -140,23 +140,23 @@ __device__ __forceinline__ void la_group(int g, int act, int &lo, int &hi) {
     hi = LA_DF + 1 + ((g + 1) * nf) / LA_NG;
 }
 // window rows: far P[c][win][j][w] (w < la_W parts), mid P[c][win][j]
-__device__ __forceinline__ float4 *la_pf(const ProcArgs &a, size_t c, int win, int j, int w, int B) {
+__device__ __forceinline__ float4 *la_pf(const ProcArgs &a, int jb, size_t c, int win, int j, int w, int B) {
 #ifdef FFTCONV_DEBUG_BOUNDS
     if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && j >= 0 && j < LA_DF && w >= 0 && w < a.la_W)) {
         printf("BOUNDS la_pf blk %d c %d win %d j %d w %d\n", (int)blockIdx.x, (int)c, win, j, w);
         c = 0; win = 0; j = 0; w = 0;
     }
 #endif
-    return reinterpret_cast<float4 *>(a.laP + ((((c * 2 + win) * LA_DF + j) * (size_t)a.la_W + w) * (size_t)B));
+    return reinterpret_cast<float4 *>((jb ? a.laP2 : a.laP) + ((((c * 2 + win) * LA_DF + j) * (size_t)a.la_W + w) * (size_t)B));
 }
-__device__ __forceinline__ float4 *la_pm(const ProcArgs &a, size_t c, int win, int j, int B) {
+__device__ __forceinline__ float4 *la_pm(const ProcArgs &a, int jb, size_t c, int win, int j, int B) {
 #ifdef FFTCONV_DEBUG_BOUNDS
     if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && j >= 0 && j < LA_DM)) {
         printf("BOUNDS la_pm blk %d c %d win %d j %d\n", (int)blockIdx.x, (int)c, win, j);
         c = 0; win = 0; j = 0;
     }
 #endif
-    return reinterpret_cast<float4 *>(a.laPm + (((c * 2 + win) * LA_DM + j) * (size_t)B));
+    return reinterpret_cast<float4 *>((jb ? a.laPm2 : a.laPm) + (((c * 2 + win) * LA_DM + j) * (size_t)B));
 }
 
 // ---------------------------------------------------------------------------
@@ -308,9 +308,9 @@ struct LaGeo {
 // Nothing else of the step is read by an anchor (FDL ages >= 1 only, the
 // other window of each level).
 template <int LOG2B>
-__device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int c, int P, int &cur, int &act, int &win,
+__device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c, int P, int &cur, int &act, int &win,
                                                 int &d) {
-    const ProcJob &J = a.job[0];
+    const ProcJob &J = a.job[jb];
     DBG_CHECK(c >= 0 && c < a.la_channels, "anchor state blk %d c %d P %d\n", (int)blockIdx.x, c, P);
     const int4 st = J.state[c];
     const int sx = __builtin_amdgcn_readfirstlane(st.x), sy = __builtin_amdgcn_readfirstlane(st.y);
@@ -350,10 +350,10 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int c, int P,
 // Pf[win][j][w].
 // ---------------------------------------------------------------------------
 template <int LOG2B, bool NTL>
-__device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned char *smem) {
+__device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, unsigned char *smem) {
     using LG = LaGeo<LOG2B>;
     constexpr int B = LG::B, GPW = LG::GPW;
-    const ProcJob &J = a.job[0];
+    const ProcJob &J = a.job[jb];
     // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so the
     // WG_FAR workgroups of one anchor sit 8 apart -- on one XCD, whose L2
     // then serves the rows the window halves and neighbouring groups share
@@ -362,7 +362,7 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
     const int c = a.la_all > 0 ? a.la_c0 + ci : (a.la_t % LA_DF) + LA_DF * ci;
     if (c >= a.la_channels) return;  // (padding of the last XCD round)
     int cur, act, win, d;
-    if (!la_anchor_state<LOG2B>(a, c, LA_DF, cur, act, win, d)) return;
+    if (!la_anchor_state<LOG2B>(a, jb, c, LA_DF, cur, act, win, d)) return;
     if ((r / (LG::NSL * LG::WF)) * LA_JW >= d) return;  // a window slice wholly past the window
 
     constexpr int FS = LG::FS, NSL = LG::NSL;
@@ -410,28 +410,28 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int b, unsigned
                     float4 p = acc[j].get();
 #pragma unroll
                     for (int q = 1; q < GPW; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * FS + fl]);
-                    la_pf(a, c, win, h * LA_JW + j, w, B)[f] = p;
+                    la_pf(a, jb, c, win, h * LA_JW + j, w, B)[f] = p;
                 }
             }
         }
     } else {
 #pragma unroll
         for (int j = 0; j < LA_JW; ++j)
-            if (h * LA_JW + j < d) la_pf(a, c, win, h * LA_JW + j, w, B)[f] = acc[j].get();
+            if (h * LA_JW + j < d) la_pf(a, jb, c, win, h * LA_JW + j, w, B)[f] = acc[j].get();
     }
 }
 
 // Mid anchor workgroup b: channel c's mid rows DF..D1+1 (one descending chain
 // per window step), the window steps split over the lanesets.
 template <int LOG2B, bool NTL>
-__device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
+__device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int jb, int b) {
     using LG = LaGeo<LOG2B>;
     constexpr int B = LG::B, F = LG::F, JM = LG::JM;
-    const ProcJob &J = a.job[0];
+    const ProcJob &J = a.job[jb];
     const int c = a.la_all > 0 ? a.la_c0 + b : (a.la_t % LA_DM) + LA_DM * b;
     if (c >= a.la_channels) return;
     int cur, act, win, d;
-    if (!la_anchor_state<LOG2B>(a, c, LA_DM, cur, act, win, d)) return;
+    if (!la_anchor_state<LOG2B>(a, jb, c, LA_DM, cur, act, win, d)) return;
     const int tid = threadIdx.x;
     const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
     if (l * JM >= LA_DM) return;  // (more lanesets than window steps)
@@ -445,7 +445,7 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
     la_walk<LOG2B, false, false, JM, LA_UM>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, j0, cur, act);
 #pragma unroll
     for (int j = 0; j < JM; ++j)
-        if (j0 + j >= l * JM && j0 + j < d) la_pm(a, c, win, j0 + j, B)[f] = acc[j].get();
+        if (j0 + j >= l * JM && j0 + j < d) la_pm(a, jb, c, win, j0 + j, B)[f] = acc[j].get();
 }
 
 // ---------------------------------------------------------------------------
@@ -459,21 +459,29 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int b) {
 // workgroup at B <= 256: the step and anchor workgroups of a launch then fit
 // the CUs together, so the anchors' stream runs under the transform chains.
 // ---------------------------------------------------------------------------
-template <int LOG2B>
+template <int LOG2B, int XF = 0>
 struct LaStep {
     static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;
-    static constexpr int NCH = LOG2B <= 8 ? 2 : 1;           // channels per step workgroup
+    // channels per step workgroup (XF 3: A's and B's instance of one channel)
+    static constexpr int NCH = (XF == 3 || LOG2B <= 8) ? 2 : 1;
     // B <= 256: the step workgroup's helper waves (>= one laneset of F lanes
     // after the pre) also run the mid anchors of its channels, after the
     // pre, under the transform chains; B = 512 launches mid anchor workgroups
     static constexpr bool MIDIN = LOG2B <= 8;
-    // tw (2B float2) | per channel: bufA | bufB | H0 | pre (float2) | overlap | tail0 | tail1 (float)
-    static constexpr size_t ch_bytes = 4 * 8 * (size_t)B + 3 * 4 * (size_t)B;
-    static constexpr size_t chain_bytes = 16 * (size_t)B + NCH * ch_bytes;
+    // tw (the 3N/4 = 1.5B float2 the transforms index) | per channel:
+    // bufA | bufB | pre (float2) | tail0 | tail1 (float) -- H[0] and the
+    // overlap stay in the chain wave's registers (XF 3 at B = 512: 38 KB, so
+    // four workgroups fit a CU's 160 KB instead of three)
+    static constexpr size_t tw_bytes = 12 * (size_t)B;
+    static constexpr size_t ch_bytes = 3 * 8 * (size_t)B + 2 * 4 * (size_t)B;
+    static constexpr size_t chain_bytes = tw_bytes + NCH * ch_bytes;
     // the full pass's chain results (mid + NG far groups per channel) alias
     // the chain buffers (they are consumed before the chains start)
     static constexpr size_t grp_bytes = (size_t)NCH * (1 + LA_NG) * F * 16;
-    static constexpr size_t bytes = chain_bytes > grp_bytes ? chain_bytes : grp_bytes;
+    // (+ the XF 3 mix counter after the chain buffers; it may alias the
+    // full pass's results, which are consumed before the counter is set)
+    static constexpr size_t cnt_off = chain_bytes;
+    static constexpr size_t bytes = chain_bytes + 16 > grp_bytes ? chain_bytes + 16 : grp_bytes;
 };
 
 // launch timeline phase stamp k (0..3) of this wave (FFTCONV_LA_TRACE)
@@ -484,10 +492,28 @@ __device__ __forceinline__ void la_stamp(const ProcArgs &a, int k) {
     }
 }
 
+// XF 3 (crossfade A and B in one launch): a participant of the channel's mix
+// (A's chain, B's chain, the helper that walks mix_value) has stored its part
+// in LDS; the last of the three mixes the block into the output
+// (Crossfader::mix, src/crossfade_convolver.rs:75-77, 242-278) -- no
+// workgroup barrier, so the chain waves never wait for one another.
+__device__ __forceinline__ void la_xf_arrive(const ProcArgs &a, int *cnt, const float *yA, const float *yB,
+                                             const float *vtab, size_t c) {
+    wave_sync();  // this wave's LDS stores are complete
+    int old = 0;
+    if ((threadIdx.x & 63) == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != 2) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const CrossfadeMixArgs &m = a.mix;
+    float *o = a.job[0].out + c * a.job[0].out_stride;
+    for (int j = (int)(threadIdx.x & 63); j < m.n; j += 64) o[j] = mix_select(yA[j], yB[j], mix_selector(m, j, vtab));
+}
+
 template <int LOG2B, bool NTL, int NCH, int XF>
 __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, const int (&cs)[NCH],
                                         const int4 (&st)[NCH], int nvalid, unsigned char *smem) {
-    using LS = LaStep<LOG2B>;
+    using LS = LaStep<LOG2B, XF>;
     using LG = LaGeo<LOG2B>;
     constexpr int B = LS::B, F = LS::F, LPW = LS::LPW, GPW = LG::GPW, WF = LG::WF;
     constexpr int HL = LA_NT - 64 * NCH;
@@ -498,7 +524,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     constexpr size_t chb = LS::ch_bytes;
     static_assert(NCH == 1 || NCH == 2, "one or two channels per step workgroup");
     float2 *twl = reinterpret_cast<float2 *>(smem);
-    auto chan_lds = [&](int k) { return smem + 16 * (size_t)B + (size_t)k * chb; };
+    auto chan_lds = [&](int k) { return smem + LS::tw_bytes + (size_t)k * chb; };
     float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][NCHAIN][F], full pass only
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -509,6 +535,27 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     // indexing (which would put the arrays in scratch)
     auto ST = [&](int k) { return (NCH == 1 || k == 0) ? st[0] : st[NCH - 1]; };
     auto CS = [&](int k) { return (NCH == 1 || k == 0) ? cs[0] : cs[NCH - 1]; };
+    // the instance of slot k: XF 3 runs A's (job 0) and B's (job 1) instance
+    // of one channel; otherwise every slot is a channel of job 0
+    auto JK = [&](int k) -> const ProcJob & { return (XF == 3 && k == 1) ? a.job[1] : J; };
+    auto JB = [&](int k) { return (XF == 3 && k == 1) ? 1 : 0; };
+    // XF 3: A's / B's block and the mix_value walk in LDS (the two-stage add
+    // buffers, unused by a crossfade), and the mix's arrival counter
+    float *yA = reinterpret_cast<float *>(chan_lds(0) + 24 * (size_t)B), *yB = yA + B;
+    float *vtab = reinterpret_cast<float *>(chan_lds(1) + 24 * (size_t)B);  // (B + 1 floats)
+    // the chain wave's H[0] row slots and overlap samples (registers)
+    float4 h0r[F / 64];
+    float ovr[B / 64];
+    int *xcnt = reinterpret_cast<int *>(smem + LS::cnt_off);
+    // the helpers leave the next block's near sum (FLAG_NEAR) where the
+    // step's pre is the launch's critical path: B = 512 (no in-step mid
+    // anchors; the crossfade's A + B pair: helper pre 13.9 -> 9.7 us, cfg5
+    // 47.8 -> 45.8 us per step, r2j).  With in-step mid anchors (B <= 256)
+    // the far walks bound the launch and the extra helper work after the
+    // barrier lengthens the mid-anchor workgroups (cfg2 18.97 -> 19.57 us,
+    // r2j; skipping the mid-anchor channels slows their next pre instead,
+    // r2k), so those steps sum their near rows themselves.
+    auto near_next = [&](int) { return !LS::MIDIN; };
     auto fullF = [&](int k) { return !la_far_live(ST(k).w); };
     auto fullM = [&](int k) { return !la_mid_live(ST(k).w); };
     bool anyfull = false;
@@ -533,7 +580,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             if (k >= nvalid) continue;
             const int cur = __builtin_amdgcn_readfirstlane(ST(k).x), act = __builtin_amdgcn_readfirstlane(ST(k).y);
             const bool fm = fullM(k), ff = fullF(k);
-            const RowStream hs(J.H + (size_t)CS(k) * rows, bytes), xs(J.X + (size_t)CS(k) * rows, bytes);
+            const RowStream hs(JK(k).H + (size_t)CS(k) * rows, bytes), xs(JK(k).X + (size_t)CS(k) * rows, bytes);
             for (int q = l; q < NCHAIN; q += LPW) {
                 if (q == 0 ? !fm : !ff) continue;
                 int lo, hi;
@@ -580,22 +627,25 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     } else if (wave < NCH) {
         // ---- transform chain of channel k = wave: the block -> R2C -> FDL row `current`
         const int k = wave;
+        const ProcJob &JC = JK(k);
         const size_t c = (size_t)CS(k);
         const int cur = __builtin_amdgcn_readfirstlane(ST(k).x);
         DBG_CHECK(c < (size_t)a.la_channels && cur >= 0 && cur < J.S, "step chain blk %d c %d cur %d nvalid %d\n",
                   (int)blockIdx.x, (int)c, cur, nvalid);
         float2 *bufA = reinterpret_cast<float2 *>(chan_lds(k));
-        float2 *bufB = bufA + B, *h0l = bufB + B;
-        float *ovl = reinterpret_cast<float *>(h0l + 2 * B);
-        float *p0l = ovl + B, *p1l = p0l + B;
-        const float *inc = J.in + c * J.in_stride;
+        float2 *bufB = bufA + B;
+        float *p0l = reinterpret_cast<float *>(bufA + 3 * B), *p1l = p0l + B;
+        const float *inc = JC.in + c * JC.in_stride;
         dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);  // x[0..B) as packed z[0..B/2)
         for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
-        if (k == 0) dma_16b<64>(twl, a.tw, 2 * B * (int)sizeof(float2));
-        dma_16b<64>(h0l, J.H + c * rows, B * (int)sizeof(float2));
-        dma_f32<64>(ovl, J.overlap + c * B, B);
-        if (J.add0) dma_f32<64>(p0l, J.add0 + c * J.add_stride, B);
-        if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
+        if (k == 0) dma_16b<64>(twl, a.tw, (int)LS::tw_bytes);
+        if (XF == 3 && k == 0 && lane == 0) *xcnt = 0;  // (visible to all after the barrier below)
+#pragma unroll
+        for (int i = 0; i < F / 64; ++i) h0r[i] = reinterpret_cast<const float4 *>(JC.H + c * rows)[lane + 64 * i];
+#pragma unroll
+        for (int i = 0; i < B / 64; ++i) ovr[i] = JC.overlap[c * B + lane + 64 * i];
+        if (JC.add0) dma_f32<64>(p0l, JC.add0 + c * JC.add_stride, B);
+        if (JC.add1) dma_f32<64>(p1l, JC.add1 + c * JC.add_stride, B);
         if constexpr (XF == 2) {
             // crossfade, B's launch (no two-stage adds): A's block and the
             // per-sample mix selectors (la_mix_walk) in p0l / p1l
@@ -609,15 +659,15 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         } else {
             wave_sync();
         }
-        if (J.tin) {  // two-stage: append the block to tail_input (:459-461)
+        if (JC.tin) {  // two-stage: append the block to tail_input (:459-461)
             const float *xb = reinterpret_cast<const float *>(bufA);
-            float *ti = J.tin + c * J.tin_stride;
+            float *ti = JC.tin + c * JC.tin_stride;
             for (int j = lane; j < B; j += 64) ti[j] = xb[j];
         }
         wave_sync();
         Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
         Q = Z == bufA ? bufB : bufA;
-        float2 *Xcur = J.X + c * rows + (size_t)cur * B;
+        float2 *Xcur = JC.X + c * rows + (size_t)cur * B;
         for (int m = lane; m < B; m += 64) {
             const float2 v = real_post<LOG2B, 64>(Z, m, twl);
             Q[m] = v;
@@ -633,41 +683,98 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             if (!task(t, k, f)) continue;
             const size_t c = (size_t)CS(k);
             const int cur = ST(k).x, act = ST(k).y, flags = ST(k).w;
-            const RowStream hs(J.H + c * rows, bytes), xs(J.X + c * rows, bytes);
-            float4 hv[LA_D1], xv[LA_D1];
+            const bool nearp = (flags & FLAG_NEAR) != 0;  // the previous step left this block's near sum
+            const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
+            float4 hv[LA_D1], xv[LA_D1], N0;
+            if (nearp) {
+                N0 = reinterpret_cast<const float4 *>(JK(k).pre + c * B)[f];
+            } else {
 #pragma unroll
-            for (int i = LA_D1; i >= 1; --i) {
-                int r = cur + i;
-                if (r >= act) r -= act;
-                hv[i - 1] = hs.ld4<false>(f * 16, i * ROWB);
-                xv[i - 1] = xs.ld4<false>(f * 16, r * ROWB);
+                for (int i = LA_D1; i >= 1; --i) {
+                    int r = cur + i;
+                    if (r >= act) r -= act;
+                    hv[i - 1] = hs.ld4<false>(f * 16, i * ROWB);
+                    xv[i - 1] = xs.ld4<false>(f * 16, r * ROWB);
+                }
             }
             float4 M, A;
             if (fullM(k)) {
                 M = Mreg[t];
             } else {
-                M = la_pm(a, c, (flags & FLAG_PWINM) ? 1 : 0, la_jm(flags), B)[f];
+                M = la_pm(a, JB(k), c, (flags & FLAG_PWINM) ? 1 : 0, la_jm(flags), B)[f];
             }
             if (fullF(k)) {
                 A = Freg[t];
             } else {
-                const float4 *P0 = la_pf(a, c, (flags & FLAG_PWIN) ? 1 : 0, la_jf(flags), 0, B);
+                const float4 *P0 = la_pf(a, JB(k), c, (flags & FLAG_PWIN) ? 1 : 0, la_jf(flags), 0, B);
                 A = P0[f];
 #pragma unroll
                 for (int w = 1; w < WF; ++w) A = vadd(A, P0[(size_t)w * F + f]);
             }
-            LaAcc acc;
-            acc.zero();
+            if (!nearp) {
+                LaAcc acc;
+                acc.zero();
 #pragma unroll
-            for (int i = LA_D1; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
-            float2 *prel = reinterpret_cast<float2 *>(chan_lds(k)) + 3 * B;
-            reinterpret_cast<float4 *>(prel)[f] = vadd(acc.get(), vadd(M, A));
+                for (int i = LA_D1; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
+                N0 = acc.get();
+            }
+            float2 *prel = reinterpret_cast<float2 *>(chan_lds(k)) + 2 * B;
+            reinterpret_cast<float4 *>(prel)[f] = vadd(N0, vadd(M, A));
+            if constexpr (TPL > 2) __builtin_amdgcn_sched_barrier(0);  // (one task's rows in flight at a time)
         }
         la_stamp(a, 0);
     }
     __syncthreads();
     la_stamp(a, 2);
     if (wave >= NCH) {
+        if constexpr (XF == 3) {
+            if (wave == NCH) {  // this call's mix_value walk (:259), one lane, then arrive
+                if (a.mix.approaching && lane == 0) {
+                    const int n = a.mix.n;
+                    const float step = a.mix.step;
+                    float v = a.mix.mix_value0;
+                    vtab[0] = v;
+                    for (int q = 1; q <= n; ++q) {  // one f32 rounding each, as the reference
+                        v = __fadd_rn(v, step);
+                        vtab[q] = v;
+                    }
+                }
+                la_xf_arrive(a, xcnt, yA, yB, vtab, (size_t)CS(0));
+            }
+        }
+        // the NEXT block's near sum, rows D1..1 in the canonical order, while
+        // the chains run their C2R: rows D1..2 meet the blocks this step's
+        // near rows met one age earlier, row 1 meets this step's block (the
+        // chain's spectrum Q, kept in LDS) -- stored in pre[] (FLAG_NEAR)
+        {
+            constexpr int QOFF = ((LOG2B / 2 + (LOG2B & 1)) & 1) ? 0 : B;  // Q = the buffer lds_cfft did not end in
+#pragma unroll
+            for (int t = 0; t < TPL; ++t) {
+                int k, f;
+                if (!task(t, k, f) || !near_next(k)) continue;
+                const size_t c = (size_t)CS(k);
+                const int cur = ST(k).x, act = ST(k).y;
+                const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
+                float4 hv[LA_D1], xv[LA_D1 - 1];
+#pragma unroll
+                for (int i = LA_D1; i >= 1; --i) {
+                    hv[i - 1] = hs.ld4<false>(f * 16, i * ROWB);
+                    if (i >= 2) {
+                        int r = cur + i - 1;
+                        if (r >= act) r -= act;
+                        xv[i - 2] = xs.ld4<false>(f * 16, r * ROWB);
+                    }
+                }
+                const float4 xq = reinterpret_cast<const float4 *>(reinterpret_cast<float2 *>(chan_lds(k)) + QOFF)[f];
+                LaAcc acc;
+                acc.zero();
+#pragma unroll
+                for (int i = LA_D1; i >= 2; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 2]);
+                acc.mac(la_ops(hv[0], f == 0), xq);
+                reinterpret_cast<float4 *>(JK(k).pre + c * B)[f] = acc.get();
+                if constexpr (TPL > 2) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
         if (a.la_probe >= 5) return;  // (timing probes 5/6: steps without their mid anchors)
         if constexpr (LS::MIDIN) {
           if (a.la_nmid == 0) {  // (FFTCONV_LA_MIDWG: mid anchors in workgroups of their own)
@@ -686,7 +793,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                     const int act = __builtin_amdgcn_readfirstlane(ST(k).y);
                     const int flags = __builtin_amdgcn_readfirstlane(ST(k).w);
                     const int win = (flags & FLAG_PWINM) ? 0 : 1, d = la_dnew((int)c, a, LA_DM);
-                    const RowStream hs(J.H + c * rows, bytes), xs(J.X + c * rows, bytes);
+                    const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
                     LaAcc acc[JMS];
 #pragma unroll
                     for (int j = 0; j < JMS; ++j) acc[j].zero();
@@ -695,7 +802,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                                                          act);
 #pragma unroll
                     for (int j = 0; j < JMS; ++j)
-                        if (j0 + j >= l * JMS && j0 + j < d) la_pm(a, c, win, j0 + j, B)[f] = acc[j].get();
+                        if (j0 + j >= l * JMS && j0 + j < d) la_pm(a, JB(k), c, win, j0 + j, B)[f] = acc[j].get();
                 }
             }
           }
@@ -705,21 +812,24 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     if (wave >= nvalid) return;
 
     const int k = wave;
+    const ProcJob &JC = JK(k);
     const size_t c = (size_t)CS(k);
     const int cur = __builtin_amdgcn_readfirstlane(ST(k).x), act = __builtin_amdgcn_readfirstlane(ST(k).y);
     const int flags = __builtin_amdgcn_readfirstlane(ST(k).w);
     float2 *bufA = reinterpret_cast<float2 *>(chan_lds(k));
-    float2 *h0l = bufA + 2 * B, *prel = bufA + 3 * B;
-    float *ovl = reinterpret_cast<float *>(bufA + 4 * B);
-    float *p0l = ovl + B, *p1l = p0l + B;
-    float *outc = J.out + c * J.out_stride;
-    float *ovc = J.overlap + c * B;
+    float2 *prel = bufA + 2 * B;
+    float *p0l = reinterpret_cast<float *>(bufA + 3 * B), *p1l = p0l + B;
+    // (XF 3: this instance's block goes to LDS, the mix writes the output)
+    float *outc = XF == 3 ? (k == 0 ? yA : yB) : JC.out + c * JC.out_stride;
+    float *ovc = JC.overlap + c * B;
     // crossfade, B's launch: out = mix(A's block, this block) (:75-77)
     bool bad = false;  // conv = pre + X (.) H[0] (:256-261), then the C2R error check
     la_stamp(a, 3);
-    for (int f = lane; f < F; f += 64) {
+#pragma unroll
+    for (int i = 0; i < F / 64; ++i) {
+        const int f = lane + 64 * i;
         const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
-                                   reinterpret_cast<const float4 *>(h0l)[f], f);
+                                   h0r[i], f);
         reinterpret_cast<float4 *>(Z)[f] = cv;
         if (f == 0 && !slot0_finite(cv)) bad = true;
     }
@@ -728,14 +838,18 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     const int keep = flags & ~(FLAG_INBUF | FLAG_PRE | LA_MASK | SEQ_MASK);
     const int tag = a.la_seq << SEQ_SHIFT;
     if (!err) {
-        for (int m = lane; m < B; m += 64) Q[m] = real_pre<LOG2B, 64>(Z, m, twl);
+        // (the C2R ping-pongs through prel and Z: Q -- this block's spectrum --
+        // stays intact for the helpers' next near sum)
+        for (int m = lane; m < B; m += 64) prel[m] = real_pre<LOG2B, 64>(Z, m, twl);
         wave_sync();
-        const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(Q, Z, twl));
-        for (int j = lane; j < B; j += 64) {  // overlap-add (:270-274) + two-stage adds (:439-454)
-            float v = y[j] * invN + ovl[j];
-            if (J.add0) {
+        const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(prel, Z, twl));
+#pragma unroll
+        for (int i = 0; i < B / 64; ++i) {  // overlap-add (:270-274) + two-stage adds (:439-454)
+            const int j = lane + 64 * i;
+            float v = y[j] * invN + ovr[i];
+            if (JC.add0) {
                 v += p0l[j];
-                if (J.add1) v += p1l[j];
+                if (JC.add1) v += p1l[j];
             }
             if constexpr (XF == 2) v = mix_select(p0l[j], v, p1l[j]);
             outc[j] = v;
@@ -743,7 +857,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         }
         if (lane == 0) {
             const int curp = cur > 0 ? cur - 1 : act - 1;  // :287-291
-            int nf = (keep ^ FLAG_REV) | tag;
+            int nf = (keep ^ FLAG_REV) | tag | (near_next(k) ? FLAG_NEAR : 0);  // (the helpers stored it)
             // far window: open (a far anchor this launch), advance, or drop
             if (la_sched((int)c, a, LA_DF))
                 nf = (nf ^ FLAG_PWIN) | FLAG_LA | ((la_dnew((int)c, a, LA_DF) - 1) << LA_D_SHIFT);
@@ -754,25 +868,26 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 nf = (nf ^ FLAG_PWINM) | FLAG_LAM | ((la_dnew((int)c, a, LA_DM) - 1) << LA_DM_SHIFT);
             else if (la_mid_live(flags))
                 nf |= FLAG_LAM | ((la_jm(flags) + 1) << LA_JM_SHIFT) | ((la_dm(flags) - 1) << LA_DM_SHIFT);
-            J.state[c] = make_int4(curp, act, 0, nf);
+            JC.state[c] = make_int4(curp, act, 0, nf);
         }
     } else {
         // output.fill(0); return (:264-267): the block stays in the input
         // buffer, fill / current unchanged; the windows are dropped
-        const float *inc = J.in + c * J.in_stride;
-        float *ibc = J.inbuf + c * B;
+        const float *inc = JC.in + c * JC.in_stride;
+        float *ibc = JC.inbuf + c * B;
         for (int j = lane; j < B; j += 64) {
             float v = 0.f;
-            if (J.add0) {
+            if (JC.add0) {
                 v += p0l[j];
-                if (J.add1) v += p1l[j];
+                if (JC.add1) v += p1l[j];
             }
             if constexpr (XF == 2) v = mix_select(p0l[j], v, p1l[j]);
             ibc[j] = inc[j];  // (before the output: a caller's output may alias its input)
             outc[j] = v;
         }
-        if (lane == 0) J.state[c] = make_int4(cur, act, 0, keep | FLAG_INBUF | tag);
+        if (lane == 0) JC.state[c] = make_int4(cur, act, 0, keep | FLAG_INBUF | tag);
     }
+    if constexpr (XF == 3) la_xf_arrive(a, xcnt, yA, yB, vtab, c);
 }
 
 // a channel off the lookahead path (partial block, buffered input, short
@@ -810,7 +925,42 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
     }
 }
 
-// grid: [far anchors | mid anchors | step workgroups] (or the steps first)
+// XF 3: channel c of A or B off the lookahead path -- both instances take the
+// generic step (out to buf_a / buf_b), then the workgroup walks mix_value and
+// mixes (the same arithmetic as the lookahead mix)
+template <int LOG2B, bool NTL>
+__device__ __attribute__((noinline)) void la_fallback_xf(const ProcArgs *ap, int c, unsigned char *smem) {
+    const ProcArgs &a = *ap;
+    const CrossfadeMixArgs m = a.mix;
+    ProcJob Ja = a.job[0], Jb = a.job[1];
+    Ja.out = const_cast<float *>(m.buf_a);
+    Ja.out_stride = m.buf_stride;
+    Jb.out = const_cast<float *>(m.buf_b);
+    Jb.out_stride = m.buf_stride;
+    const int4 sa = Ja.state[c], sb = Jb.state[c];
+    process_job<LOG2B, LA_NT, false, NTL>(a, Ja, (size_t)c, sa, smem);
+    __syncthreads();
+    process_job<LOG2B, LA_NT, false, NTL>(a, Jb, (size_t)c, sb, smem);
+    __syncthreads();
+    float *t = reinterpret_cast<float *>(smem);
+    if (m.approaching) {
+        if (threadIdx.x == 0) {
+            float v = m.mix_value0;
+            t[0] = v;
+            for (int q = 1; q <= m.n; ++q) {
+                v = __fadd_rn(v, m.step);
+                t[q] = v;
+            }
+        }
+        __syncthreads();
+    }
+    const float *ya = m.buf_a + (size_t)c * m.buf_stride, *yb = m.buf_b + (size_t)c * m.buf_stride;
+    float *o = a.job[0].out + (size_t)c * a.job[0].out_stride;
+    for (int j = threadIdx.x; j < m.n; j += LA_NT) o[j] = mix_select(ya[j], yb[j], mix_selector(m, j, t));
+}
+
+// grid: [far anchors | mid anchors | step workgroups] (or the steps first);
+// XF 3: [A's far | B's far | A's mid | B's mid | one workgroup per channel]
 constexpr int LA_XWG = 8;  // A's launch: leading workgroups (the first writes the mix_value walk)
 
 // crossfade, A's launch: per-sample mix selectors of this call for B's
@@ -844,8 +994,37 @@ __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsign
 // 2 = B's launch, whose steps mix A's block with their own
 template <int LOG2B, bool NTL, int XF>
 __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char *smem) {
-    using LS = LaStep<LOG2B>;
+    using LS = LaStep<LOG2B, XF>;
     constexpr int NCH = LS::NCH;
+    if constexpr (XF == 3) {
+        const int nf = a.la_nfar, nm = a.la_nmid;
+        // (la_steps_first: the channels' step workgroups lead the grid -- the
+        // latency-critical chains get the CUs first, the anchors fill in)
+        int b = (int)blockIdx.x;
+        if (a.la_steps_first) b = b < a.la_channels ? b + 2 * (nf + nm) : b - a.la_channels;
+        if (b < 2 * nf) {  // (nf is a multiple of 8: B's far anchors keep the XCD placement)
+            la_anchor_far<LOG2B, NTL>(a, b >= nf ? 1 : 0, b >= nf ? b - nf : b, smem);
+            return;
+        }
+        if (b < 2 * (nf + nm)) {
+            const int bm = b - 2 * nf;
+            la_anchor_mid<LOG2B, NTL>(a, bm >= nm ? 1 : 0, bm >= nm ? bm - nm : bm);
+            return;
+        }
+        const int c = b - 2 * (nf + nm);
+        if (c >= a.la_channels) return;
+        const int4 va = a.job[0].state[c], vb = a.job[1].state[c];
+        const int4 st[2] = {make_int4(__builtin_amdgcn_readfirstlane(va.x), __builtin_amdgcn_readfirstlane(va.y),
+                                      __builtin_amdgcn_readfirstlane(va.z), __builtin_amdgcn_readfirstlane(va.w)),
+                            make_int4(__builtin_amdgcn_readfirstlane(vb.x), __builtin_amdgcn_readfirstlane(vb.y),
+                                      __builtin_amdgcn_readfirstlane(vb.z), __builtin_amdgcn_readfirstlane(vb.w))};
+        const int cs[2] = {c, c};
+        if (la_eligible<LOG2B>(st[0], a.job[0].n) && la_eligible<LOG2B>(st[1], a.job[1].n))
+            la_step<LOG2B, NTL, 2, 3>(a, a.job[0], cs, st, 2, smem);
+        else
+            la_fallback_xf<LOG2B, NTL>((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), c, smem);
+        return;
+    }
     if constexpr (XF == 1) {
         // 8 extra workgroups at the front of the grid (one per XCD: the far
         // anchors' XCD placement behind them is unchanged); the first walks,
@@ -862,9 +1041,9 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
     if (ba >= 0 && ba < nanchor) {
         if (a.la_probe != 1 && a.la_probe != 6) {
             if (ba < a.la_nfar) {
-                if (a.la_probe != 4) la_anchor_far<LOG2B, NTL>(a, ba, smem);
+                if (a.la_probe != 4) la_anchor_far<LOG2B, NTL>(a, 0, ba, smem);
             } else if (a.la_probe != 3) {
-                la_anchor_mid<LOG2B, NTL>(a, ba - a.la_nfar);
+                la_anchor_mid<LOG2B, NTL>(a, 0, ba - a.la_nfar);
             }
         }
         return;
@@ -894,6 +1073,11 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
 // the role of workgroup blockIdx.x in a lookahead launch (for the timeline)
 template <int XF>
 __device__ __forceinline__ int la_role(const ProcArgs &a) {
+    if (XF == 3) {
+        int b = (int)blockIdx.x;
+        if (a.la_steps_first) b = b < a.la_channels ? b + 2 * (a.la_nfar + a.la_nmid) : b - a.la_channels;
+        return b < 2 * a.la_nfar ? 0 : (b < 2 * (a.la_nfar + a.la_nmid) ? 1 : 2);
+    }
     if (XF == 1 && blockIdx.x < LA_XWG) return 4;  // mix walk
     const int nanchor = a.la_nfar + a.la_nmid;
     const int nstep = (int)gridDim.x - nanchor - (XF == 1 ? LA_XWG : 0);

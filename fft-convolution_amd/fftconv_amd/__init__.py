@@ -42,6 +42,10 @@ SIGNATURES = {
     "fftconv_device_count": (_i, []),
     "fftconv_complex_size": (_sz, [_sz]),
     "fftconv_compute_tail_block_size": (_sz, [_sz, _sz]),
+    "fftconv_fft_forward": (_i, [_i, _sz, _sz, _vp, _sz, _vp, _sz, _vp]),
+    "fftconv_fft_inverse": (_i, [_i, _sz, _sz, _vp, _sz, _vp, _sz, _vp, _vp]),
+    "fftconv_fft_forward_host": (_i, [_i, _sz, _sz, _fp, _fp]),
+    "fftconv_fft_inverse_host": (_i, [_i, _sz, _sz, _fp, _fp, C.POINTER(_i)]),
     "fftconv_set_kernel_variant": (_i, [_i]),
     "fftconv_get_kernel_variant": (_i, []),
     "fftconv_set_pipeline_lag": (_i, [_i]),
@@ -63,6 +67,7 @@ SIGNATURES = {
     "fftconv_uniform_lookahead_parts": (_i, [_vp]),
     "fftconv_uniform_block_size": (_sz, [_vp]),
     "fftconv_uniform_seg_count": (_sz, [_vp]),
+    "fftconv_uniform_ir_spectrum": (_i, [_vp, _sz, _sz, _fp]),
     "fftconv_uniform_channel_state": (_i, [_vp, _sz, C.POINTER(_sz)]),
     "fftconv_twostage_init": (_vp, [_fp, _sz, _sz, _sz]),
     "fftconv_twostage_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
@@ -195,6 +200,48 @@ def device_count() -> int:
     return int(lib().fftconv_device_count())
 
 
+class Fft:
+    """Fft (src/fft_convolver.rs:7-50) of length n on the GPU: realfft's
+    R2C / C2R (forward unnormalised, inverse / n), batched over rows."""
+
+    def __init__(self, length: int, device: int = 0):
+        self.n = int(length)
+        self.device = device
+
+    def forward(self, x) -> np.ndarray:
+        """[rows][n] (or [n]) reals -> complex64 [rows][n/2 + 1]."""
+        x = _f32(x)
+        flat = x.ndim == 1
+        x2 = x.reshape(-1, self.n)
+        out = np.zeros((x2.shape[0], self.n + 2), np.float32)
+        _check(lib().fftconv_fft_forward_host(self.device, self.n, x2.shape[0], _p(x2), _p(out)))
+        out = out.view(np.complex64)
+        return out[0] if flat else out
+
+    def inverse(self, spec):
+        """complex [rows][n/2 + 1] -> ([rows][n] reals / n, per-row
+        FftError::InputValues flags (non-zero DC / Nyquist imaginary part))."""
+        z = np.ascontiguousarray(np.asarray(spec, np.complex64))
+        flat = z.ndim == 1
+        z2 = z.reshape(-1, self.n // 2 + 1)
+        zf = np.ascontiguousarray(z2).view(np.float32)
+        out = np.zeros((z2.shape[0], self.n), np.float32)
+        st = np.zeros(z2.shape[0], np.int32)
+        _check(lib().fftconv_fft_inverse_host(self.device, self.n, z2.shape[0], _p(zf), _p(out),
+                                              st.ctypes.data_as(C.POINTER(_i))))
+        return (out[0], bool(st[0])) if flat else (out, st.astype(bool))
+
+    def forward_device(self, d_in: int, in_stride: int, d_out: int, out_stride: int, rows: int, stream: int = 0):
+        _check(lib().fftconv_fft_forward(self.device, self.n, rows, C.c_void_p(d_in), in_stride, C.c_void_p(d_out),
+                                         out_stride, C.c_void_p(stream) if stream else None))
+
+    def inverse_device(self, d_in: int, in_stride: int, d_out: int, out_stride: int, rows: int, d_status: int = 0,
+                       stream: int = 0):
+        _check(lib().fftconv_fft_inverse(self.device, self.n, rows, C.c_void_p(d_in), in_stride, C.c_void_p(d_out),
+                                         out_stride, C.c_void_p(d_status) if d_status else None,
+                                         C.c_void_p(stream) if stream else None))
+
+
 def _responses(responses, channels):
     r = _f32(responses)
     if r.ndim == 1:
@@ -299,6 +346,12 @@ class FFTConvolver(_Base):
         """Anchor workgroups per channel of the lookahead step (0 = not used)."""
         return int(lib().fftconv_uniform_lookahead_parts(self._h))
 
+    def ir_spectrum(self, channel: int, segment: int) -> np.ndarray:
+        """segments_ir[segment] of a channel: complex64[B + 1]."""
+        out = np.zeros(2 * (self.block_size + 1), np.float32)
+        _check(lib().fftconv_uniform_ir_spectrum(self._h, channel, segment, _p(out)))
+        return out.view(np.complex64)
+
     def channel_state(self, channel: int = 0):
         """(current, active_seg_count, input_buffer_fill)."""
         out = (C.c_size_t * 3)()
@@ -390,7 +443,7 @@ class CrossfadeConvolver(_Base):
 
 
 __all__ = [
-    "FFTConvolver", "TwoStageFFTConvolver", "CrossfadeConvolver", "ConvolutionPanic",
+    "Fft", "FFTConvolver", "TwoStageFFTConvolver", "CrossfadeConvolver", "ConvolutionPanic",
     "NotImplementedInReference", "DeviceError", "complex_size", "compute_tail_block_size", "device_count",
     "lib", "LIB_PATH", "SIGNATURES",
 ]

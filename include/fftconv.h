@@ -58,6 +58,25 @@ const char *fftconv_last_error(void);            /* thread-local, "" if none */
 int fftconv_device_count(void);                   /* visible HIP devices, 0 if none */
 size_t fftconv_complex_size(size_t size);         /* src/fft_convolver.rs:52-54 */
 size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /* :520-526 */
+
+/* ---- Fft (src/fft_convolver.rs:7-50) ----------------------------------- */
+/* The reference's public real FFT (realfft's RealToComplex / ComplexToReal of
+ * length n) as batched device transforms -- the convolver's own kernels, so a
+ * spectrum here is bit-identical to the convolver's.  n: power of two in
+ * 2..16384.  Forward (Fft::forward :36-39): rows of n reals -> n/2+1 bins,
+ * interleaved (re, im), unnormalised, DC / Nyquist imaginary parts 0.
+ * Inverse (Fft::inverse :41-49): n/2+1 bins -> n reals divided by n;
+ * d_status[row] (optional) = 1 where realfft returns FftError::InputValues
+ * (non-zero DC / Nyquist imaginary part; the transform runs with those parts
+ * as 0).  Strides in floats; enqueued on `hip_stream` (NULL = legacy stream). */
+int fftconv_fft_forward(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
+                        size_t out_stride, void *hip_stream);
+int fftconv_fft_inverse(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
+                        size_t out_stride, int *d_status, void *hip_stream);
+/* Host-memory forms, rows packed ([rows][n] reals, [rows][n+2] bin floats);
+ * synchronous (temporary device buffers: not for the real-time path). */
+int fftconv_fft_forward_host(int device, size_t n, size_t rows, const float *input, float *output);
+int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *input, float *output, int *status);
 /* Tuning knob (process-wide): spectral-MAC scan variant of the fused kernel,
  * -1 = automatic (default: nontemporal loads when the per-step H+X stream
  * exceeds the Infinity Cache, plain loads otherwise -- the load policy never
@@ -148,6 +167,9 @@ size_t fftconv_uniform_channels(const fftconv_uniform *h);
 int fftconv_uniform_lookahead_parts(const fftconv_uniform *h);
 size_t fftconv_uniform_block_size(const fftconv_uniform *h);   /* next_power_of_two(max_block_size) */
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h);
+/* segments_ir[segment] of one channel (src/fft_convolver.rs:92): B+1 bins,
+ * interleaved (re, im), into host `out` ((B+1)*2 floats) */
+int fftconv_uniform_ir_spectrum(const fftconv_uniform *h, size_t channel, size_t segment, float *out);
 /* copies {current, active_seg_count, input_buffer_fill} of one channel */
 int fftconv_uniform_channel_state(const fftconv_uniform *h, size_t channel, size_t out3[3]);
 

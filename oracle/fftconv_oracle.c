@@ -163,6 +163,30 @@ static int rfft_inverse(const rfft_t *f, cpx *in, float *x) {
     return bad;
 }
 
+/* Fft::forward / Fft::inverse (src/fft_convolver.rs:36-49) of one row of even
+ * length n, for the tests (the checker of fftconv_fft_*).  Complex arrays are
+ * n/2+1 interleaved (re, im).  The inverse divides by n like the reference
+ * (:44-46) and returns 1 where realfft returns FftError::InputValues. */
+int oracle_rfft_forward(size_t n, const float *x, float *out) {
+    rfft_t f;
+    if (n == 0 || (n & 1) || rfft_init(&f, n)) return -1;
+    rfft_forward(&f, x, (cpx *)out);
+    rfft_free(&f);
+    return 0;
+}
+int oracle_rfft_inverse(size_t n, const float *in, float *x) {
+    rfft_t f;
+    if (n == 0 || (n & 1) || rfft_init(&f, n)) return -1;
+    cpx *tmp = (cpx *)malloc((n / 2 + 1) * sizeof(cpx));
+    if (!tmp) { rfft_free(&f); return -1; }
+    memcpy(tmp, in, (n / 2 + 1) * sizeof(cpx));
+    int bad = rfft_inverse(&f, tmp, x);
+    for (size_t i = 0; i < n; i++) x[i] /= (float)n; /* :44-46 */
+    free(tmp);
+    rfft_free(&f);
+    return bad;
+}
+
 /* ------------------------------------------------------------------------ */
 /* primitives: src/fft_convolver.rs:52-84                                    */
 /* ------------------------------------------------------------------------ */

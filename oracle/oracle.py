@@ -74,6 +74,8 @@ def lib():
             "oracle_xfader_state": (C.c_int, [vp]),
             "oracle_bench_uniform": (C.c_double, [_sz, _sz, _sz, _sz, _sz, _sz, C.c_uint64]),
             "oracle_bench": (C.c_double, [C.c_int, _sz, _sz, _sz, _sz, _sz, _sz, C.c_uint64, _sz]),
+            "oracle_rfft_forward": (C.c_int, [_sz, _f32p, _f32p]),
+            "oracle_rfft_inverse": (C.c_int, [_sz, _f32p, _f32p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -278,6 +280,28 @@ class Crossfader(_Handle):
 
 def bench_uniform(channels, block, ir_len, nblocks, warm, threads, seed=1234) -> float:
     return float(lib().oracle_bench_uniform(channels, block, ir_len, nblocks, warm, threads, seed))
+
+
+def rfft_forward(x) -> np.ndarray:
+    """Fft::forward (src/fft_convolver.rs:36-39): unnormalised R2C of an even
+    length row -> complex64[n/2 + 1] (the restatement of realfft's algorithm)."""
+    x = _f32(x)
+    out = np.zeros(x.size + 2, np.float32)
+    if lib().oracle_rfft_forward(x.size, _ptr(x), _ptr(out)):
+        raise ValueError("length must be even and > 0")
+    return out.view(np.complex64)
+
+
+def rfft_inverse(spec, n: int):
+    """Fft::inverse (src/fft_convolver.rs:41-49): C2R of n/2+1 bins, / n.
+    Returns (x, input_error): realfft's FftError::InputValues when DC or
+    Nyquist has a non-zero imaginary part (the output is computed anyway)."""
+    z = np.ascontiguousarray(np.asarray(spec, np.complex64)).view(np.float32)
+    x = np.zeros(n, np.float32)
+    rc = lib().oracle_rfft_inverse(n, _ptr(z), _ptr(x))
+    if rc < 0:
+        raise ValueError("length must be even and > 0")
+    return x, bool(rc)
 
 
 BENCH_KINDS = {"uniform": 0, "twostage": 1, "crossfade": 2}
