@@ -51,6 +51,7 @@ def algorithmic_bytes_per_channel_block(B: int, L: int) -> int:
 
 
 LA_D1, LA_DM, LA_DF = 5, 5, 32  # lookahead levels (fft-convolution_amd/csrc/la.hpp)
+LA_NEAR_NEXT_MIN_B = 512  # la.hpp near_next(): B > 256 (no in-step mid anchors) stores the next near sum
 
 
 def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
@@ -63,13 +64,16 @@ def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
       near rows (step): H[1..D1] and the last D1 blocks: 8K * 2 D1;
       window rows written by the anchors and read by the steps: 16K (parts + 1);
       the new X row, H[0], in, out, overlap r/w: 16K + 16B.
+    At B >= 512 the helpers also store the next block's near sum (la.hpp
+    near_next): per block one more row read and one written, one FDL row
+    fewer read (this block's spectrum comes from LDS): + 8K.
     cfg2 (parts 1): 82,750 B, against 779,208 B for the reference's
     algorithm (every block streams all S rows of H and of the FDL)."""
     S = -(-L // B)
     K = B + 1
     far = 8 * K * (2 * S - LA_DF - 3) // LA_DF
     mid = 8 * K * (2 * LA_DF - LA_D1 - 1) // LA_DM
-    near = 8 * K * 2 * LA_D1
+    near = 8 * K * 2 * LA_D1 + (8 * K if B >= LA_NEAR_NEXT_MIN_B else 0)
     return far + mid + near + 16 * K * (parts + 1) + 16 * K + 16 * B
 
 

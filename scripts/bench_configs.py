@@ -223,7 +223,8 @@ def main():
         out.append({"config": "cfg5 CrossfadeConvolver, update every 128 blocks", "channels": C, "block": B,
                     "ir": L, "steps": a.steps5, "MSamples_s": round(samples / t / 1e6, 2),
                     "us_per_step": round(t / a.steps5 * 1e6, 3),
-                    "path": "lookahead step: A launch (+ mix gain walk), B launch with the mix in its epilogue" if la else "full-sum pair launch",
+                    "path": ("lookahead step: ONE launch per call (A's and B's anchors; per channel one workgroup "
+                             "with A's and B's chains, mixed in LDS)") if la else "full-sum pair launch",
                     "algorithmic_GBs_incl_updates": round(samples * per_sample / t / 1e9, 1),
                     "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
                     "bytes_per_sample": round(per_sample, 1),
