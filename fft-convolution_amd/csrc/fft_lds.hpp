@@ -58,6 +58,84 @@ __device__ __forceinline__ void stage_sync() {
     else __syncthreads();
 }
 
+// One radix-4 Stockham stage s (sub-transform length Ns = 4^s so far) of an
+// M-point complex FFT over LDS, by NT threads; `tw` is the W_N table, N = 2M.
+// The four outputs of butterfly j go to base + q Ns.  For Ns < 16 the 16
+// lanes of a ds_write_b64 group would hit 4 bank pairs (writes at stride 4
+// Ns float2); each lane therefore stores its outputs in the order
+// q = (r + j/4) mod 4, r = 0..3, which spreads every store instruction over
+// all 16 bank pairs.  Only the store order changes, not a value.
+template <int LOG2M, int NT, bool INV, int S>
+__device__ __forceinline__ void fft_stage_r4(const float2 *src, float2 *dst, const float2 *__restrict__ tw, int tid) {
+    constexpr int M = 1 << LOG2M;
+    constexpr int N = 2 * M;
+    constexpr int Ns = 1 << (2 * S);      // sub-transform length so far
+    constexpr int step = N / (Ns * 4);    // table stride for this stage
+    for (int j = tid; j < M / 4; j += NT) {
+        const int k = j & (Ns - 1);
+        float2 v0 = src[j];
+        float2 v1 = src[j + M / 4];
+        float2 v2 = src[j + M / 2];
+        float2 v3 = src[j + 3 * M / 4];
+        if constexpr (S > 0) {
+            v1 = twmul<INV>(v1, tw[k * step]);
+            v2 = twmul<INV>(v2, tw[2 * k * step]);
+            v3 = twmul<INV>(v3, tw[3 * k * step]);
+        }
+        const float2 a02 = cadd(v0, v2), s02 = csub(v0, v2);
+        const float2 a13 = cadd(v1, v3), s13 = mul_mi<INV>(csub(v1, v3));
+        const float2 o0 = cadd(a02, a13), o1 = cadd(s02, s13), o2 = csub(a02, a13), o3 = csub(s02, s13);
+        const int base = (j - k) * 4 + k;
+        if constexpr (Ns < 16) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int q = (r + (j >> 2)) & 3;
+                dst[base + q * Ns] = q == 0 ? o0 : (q == 1 ? o1 : (q == 2 ? o2 : o3));
+            }
+        } else {
+            dst[base] = o0;
+            dst[base + Ns] = o1;
+            dst[base + 2 * Ns] = o2;
+            dst[base + 3 * Ns] = o3;
+        }
+    }
+}
+// The final radix-2 stage when log2(M) is odd (Ns = M/2).
+template <int LOG2M, int NT, bool INV>
+__device__ __forceinline__ void fft_stage_r2(const float2 *src, float2 *dst, const float2 *__restrict__ tw, int tid) {
+    constexpr int M = 1 << LOG2M;
+    constexpr int N = 2 * M;
+    constexpr int Ns = M / 2;
+    constexpr int step = N / (Ns * 2);  // = 2
+    for (int j = tid; j < M / 2; j += NT) {
+        const int k = j & (Ns - 1);
+        float2 v0 = src[j];
+        float2 v1 = src[j + M / 2];
+        if constexpr (Ns > 1) v1 = twmul<INV>(v1, tw[k * step]);
+        const int base = (j - k) * 2 + k;
+        dst[base] = cadd(v0, v1);
+        dst[base + Ns] = csub(v0, v1);
+    }
+}
+
+// Stages [S0, S1) of the M-point FFT (radix-4 stages 0 .. R4-1, then the
+// radix-2 stage R4 when log2(M) is odd), ping-ponging src -> dst; returns
+// the buffer holding the result.
+template <int LOG2M, int NT, bool INV, bool WAVE, int S0, int S1>
+__device__ __forceinline__ float2 *fft_stages(float2 *src, float2 *dst, const float2 *__restrict__ tw, int tid) {
+    constexpr int R4 = LOG2M / 2;
+    if constexpr (S0 >= S1) {
+        return src;
+    } else {
+        if constexpr (S0 < R4) fft_stage_r4<LOG2M, NT, INV, S0>(src, dst, tw, tid);
+        else fft_stage_r2<LOG2M, NT, INV>(src, dst, tw, tid);
+        stage_sync<WAVE>();
+        return fft_stages<LOG2M, NT, INV, WAVE, S0 + 1, S1>(dst, src, tw, tid);
+    }
+}
+template <int LOG2M>
+constexpr int fft_nstages() { return LOG2M / 2 + (LOG2M & 1); }
+
 // M-point complex FFT (M = 2^LOG2M) over LDS, executed by NT threads.
 // Input in buf0; returns the buffer that holds the naturally ordered result
 // (buf0 or buf1).  INV = unnormalised inverse (conjugate twiddles).
@@ -66,54 +144,8 @@ __device__ __forceinline__ void stage_sync() {
 // synchronising at wave level).
 template <int LOG2M, int NT, bool INV, bool WAVE = false>
 __device__ __forceinline__ float2 *lds_cfft(float2 *buf0, float2 *buf1, const float2 *__restrict__ tw) {
-    constexpr int M = 1 << LOG2M;
-    constexpr int N = 2 * M;
-    constexpr int R4 = LOG2M / 2;
-    float2 *src = buf0;
-    float2 *dst = buf1;
     const int tid = WAVE ? (int)(threadIdx.x & (NT - 1)) : (int)threadIdx.x;  // WAVE: any one wave
-#pragma unroll
-    for (int s = 0; s < R4; ++s) {
-        const int Ns = 1 << (2 * s);        // sub-transform length so far
-        const int step = N / (Ns * 4);      // table stride for this stage
-        for (int j = tid; j < M / 4; j += NT) {
-            const int k = j & (Ns - 1);
-            float2 v0 = src[j];
-            float2 v1 = src[j + M / 4];
-            float2 v2 = src[j + M / 2];
-            float2 v3 = src[j + 3 * M / 4];
-            if (s > 0) {
-                v1 = twmul<INV>(v1, tw[k * step]);
-                v2 = twmul<INV>(v2, tw[2 * k * step]);
-                v3 = twmul<INV>(v3, tw[3 * k * step]);
-            }
-            const float2 a02 = cadd(v0, v2), s02 = csub(v0, v2);
-            const float2 a13 = cadd(v1, v3), s13 = mul_mi<INV>(csub(v1, v3));
-            const int base = (j - k) * 4 + k;
-            dst[base] = cadd(a02, a13);
-            dst[base + Ns] = cadd(s02, s13);
-            dst[base + 2 * Ns] = csub(a02, a13);
-            dst[base + 3 * Ns] = csub(s02, s13);
-        }
-        stage_sync<WAVE>();
-        float2 *t = src; src = dst; dst = t;
-    }
-    if constexpr ((LOG2M & 1) != 0) {
-        constexpr int Ns = M / 2;
-        constexpr int step = N / (Ns * 2);  // = 2
-        for (int j = tid; j < M / 2; j += NT) {
-            const int k = j & (Ns - 1);
-            float2 v0 = src[j];
-            float2 v1 = src[j + M / 2];
-            if constexpr (Ns > 1) v1 = twmul<INV>(v1, tw[k * step]);
-            const int base = (j - k) * 2 + k;
-            dst[base] = cadd(v0, v1);
-            dst[base + Ns] = csub(v0, v1);
-        }
-        stage_sync<WAVE>();
-        float2 *t = src; src = dst; dst = t;
-    }
-    return src;
+    return fft_stages<LOG2M, NT, INV, WAVE, 0, fft_nstages<LOG2M>()>(buf0, buf1, tw, tid);
 }
 
 // Post-twiddle: packed real spectrum from the complex FFT Z of the packed
@@ -143,6 +175,109 @@ __device__ __forceinline__ float2 real_pre(const float2 *X, int k, const float2 
     const float2 e = cadd(a, b);
     const float2 o = cmulc(csub(a, b), tw[k]);
     return make_float2(e.x - o.y, e.y + o.x);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-level transforms of the step chain (one wave per transform, M >= 128):
+// the ends of the R2C / C2R exchange data across the wavefront by __shfl
+// instead of an LDS round trip.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float2 shfl2(float2 v, int src) {
+    return make_float2(__shfl(v.x, src, 64), __shfl(v.y, src, 64));
+}
+// realfft's post-twiddle of bin k from Z[k] (a) and Z[M-k] (zb): real_post
+__device__ __forceinline__ float2 real_post_pair(float2 a, float2 zb, int k, const float2 *__restrict__ tw) {
+    if (k == 0) return make_float2(a.x + a.y, a.x - a.y);
+    const float2 b = make_float2(zb.x, -zb.y);
+    const float2 e = make_float2((a.x + b.x) * 0.5f, (a.y + b.y) * 0.5f);
+    const float2 o = make_float2((a.y - b.y) * 0.5f, -(a.x - b.x) * 0.5f);
+    return cadd(e, cmul(tw[k], o));
+}
+
+// R2C of the packed block in buf0 (one wave): every stage but the last
+// through LDS, the last stage in registers -- lane L then holds Z[j + q QS]
+// for its butterflies j = L + 64 i -- and the post-twiddle pairs bin k with
+// bin M - k, which sits in lane (64 - L) mod 64 at butterfly NJ-1-i, output
+// NQ-1-q (lane 0: its own registers): one __shfl per bin, no LDS round trip
+// and no wave barrier.  Same butterflies and post-twiddle as lds_cfft +
+// real_post (bit-identical).  Writes the packed spectrum to q (LDS; must not
+// be the buffer the last LDS stage ended in, fft_r2c_q_is_buf1) and g (HBM).
+template <int LOG2M>
+constexpr bool fft_r2c_q_is_buf1() { return ((fft_nstages<LOG2M>() - 1) & 1) == 0; }
+template <int LOG2M>
+__device__ __forceinline__ void wave_r2c_post(float2 *buf0, float2 *buf1, const float2 *__restrict__ tw, float2 *q,
+                                              float2 *g) {
+    constexpr int M = 1 << LOG2M;
+    constexpr bool R2 = (LOG2M & 1) != 0;     // last stage radix-2 (else radix-4, Ns = M/4)
+    constexpr int NQ = R2 ? 2 : 4;             // outputs per butterfly
+    constexpr int QS = R2 ? M / 2 : M / 4;     // index stride between them
+    constexpr int NJ = QS / 64;                // butterflies per lane
+    static_assert(NJ >= 1 && LOG2M >= 3, "wave transforms: M >= 128");
+    const int lane = (int)(threadIdx.x & 63);
+    const float2 *src = fft_stages<LOG2M, 64, false, true, 0, fft_nstages<LOG2M>() - 1>(buf0, buf1, tw, lane);
+    float2 z[NJ][NQ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+        const int j = lane + 64 * i;  // (k = j: the last stage has Ns = QS; table stride 2)
+        if constexpr (R2) {
+            const float2 v0 = src[j];
+            const float2 v1 = twmul<false>(src[j + M / 2], tw[2 * j]);
+            z[i][0] = cadd(v0, v1);
+            z[i][1] = csub(v0, v1);
+        } else {
+            const float2 v0 = src[j];
+            const float2 v1 = twmul<false>(src[j + M / 4], tw[2 * j]);
+            const float2 v2 = twmul<false>(src[j + M / 2], tw[4 * j]);
+            const float2 v3 = twmul<false>(src[j + 3 * M / 4], tw[6 * j]);
+            const float2 a02 = cadd(v0, v2), s02 = csub(v0, v2);
+            const float2 a13 = cadd(v1, v3), s13 = mul_mi<false>(csub(v1, v3));
+            z[i][0] = cadd(a02, a13);
+            z[i][1] = cadd(s02, s13);
+            z[i][2] = csub(a02, a13);
+            z[i][3] = csub(s02, s13);
+        }
+    }
+    const int mirror = (64 - lane) & 63;
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+            const int k = lane + 64 * i + qq * QS;
+            float2 b = shfl2(z[NJ - 1 - i][NQ - 1 - qq], mirror);
+            if (lane == 0) b = i == 0 ? z[0][(NQ - qq) % NQ] : z[(NJ - i) % NJ][NQ - 1 - qq];
+            const float2 v = real_post_pair(z[i][qq], b, k, tw);
+            q[k] = v;
+            g[k] = v;
+        }
+    }
+}
+
+// C2R of the packed spectrum X (LDS, one wave): realfft's pre-twiddle fused
+// with the first radix-4 stage -- lane L's four stage-0 inputs are its own
+// pre-twiddled bins j + q M/4, so they never go through LDS -- then the other
+// stages b0 <-> b1 (b1 may be X's buffer).  Bit-identical to real_pre +
+// lds_cfft<INV>.  Returns the result (2M reals, not yet scaled by 1/N).
+template <int LOG2M>
+__device__ __forceinline__ const float *wave_c2r(const float2 *X, float2 *b0, float2 *b1,
+                                                 const float2 *__restrict__ tw) {
+    constexpr int M = 1 << LOG2M;
+    const int lane = (int)(threadIdx.x & 63);
+    for (int j = lane; j < M / 4; j += 64) {
+        const float2 v0 = real_pre<LOG2M, 64>(X, j, tw);
+        const float2 v1 = real_pre<LOG2M, 64>(X, j + M / 4, tw);
+        const float2 v2 = real_pre<LOG2M, 64>(X, j + M / 2, tw);
+        const float2 v3 = real_pre<LOG2M, 64>(X, j + 3 * M / 4, tw);
+        const float2 a02 = cadd(v0, v2), s02 = csub(v0, v2);
+        const float2 a13 = cadd(v1, v3), s13 = mul_mi<true>(csub(v1, v3));
+        const float2 o0 = cadd(a02, a13), o1 = cadd(s02, s13), o2 = csub(a02, a13), o3 = csub(s02, s13);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // (stage 0: conflict-free store order, fft_stage_r4)
+            const int qq = (r + (j >> 2)) & 3;
+            b0[4 * j + qq] = qq == 0 ? o0 : (qq == 1 ? o1 : (qq == 2 ? o2 : o3));
+        }
+    }
+    wave_sync();
+    return reinterpret_cast<const float *>(fft_stages<LOG2M, 64, true, true, 1, fft_nstages<LOG2M>()>(b0, b1, tw, lane));
 }
 
 }  // namespace fftconv

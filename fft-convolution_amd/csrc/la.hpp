@@ -665,14 +665,12 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             for (int j = lane; j < B; j += 64) ti[j] = xb[j];
         }
         wave_sync();
-        Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
-        Q = Z == bufA ? bufB : bufA;
-        float2 *Xcur = JC.X + c * rows + (size_t)cur * B;
-        for (int m = lane; m < B; m += 64) {
-            const float2 v = real_post<LOG2B, 64>(Z, m, twl);
-            Q[m] = v;
-            Xcur[m] = v;
-        }
+        // R2C (:229-241) with the last stage and the post-twiddle in
+        // registers / across the wavefront (wave_r2c_post): the spectrum to
+        // Q (LDS) and FDL row `current` (HBM)
+        Q = fft_r2c_q_is_buf1<LOG2B>() ? bufB : bufA;
+        Z = fft_r2c_q_is_buf1<LOG2B>() ? bufA : bufB;
+        wave_r2c_post<LOG2B>(bufA, bufB, twl, Q, JC.X + c * rows + (size_t)cur * B);
         la_stamp(a, 1);
     } else {
         if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
@@ -747,7 +745,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         // near rows met one age earlier, row 1 meets this step's block (the
         // chain's spectrum Q, kept in LDS) -- stored in pre[] (FLAG_NEAR)
         {
-            constexpr int QOFF = ((LOG2B / 2 + (LOG2B & 1)) & 1) ? 0 : B;  // Q = the buffer lds_cfft did not end in
+            constexpr int QOFF = fft_r2c_q_is_buf1<LOG2B>() ? B : 0;  // (the chain's Q: wave_r2c_post)
 #pragma unroll
             for (int t = 0; t < TPL; ++t) {
                 int k, f;
@@ -838,11 +836,10 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     const int keep = flags & ~(FLAG_INBUF | FLAG_PRE | LA_MASK | SEQ_MASK);
     const int tag = a.la_seq << SEQ_SHIFT;
     if (!err) {
-        // (the C2R ping-pongs through prel and Z: Q -- this block's spectrum --
-        // stays intact for the helpers' next near sum)
-        for (int m = lane; m < B; m += 64) prel[m] = real_pre<LOG2B, 64>(Z, m, twl);
-        wave_sync();
-        const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(prel, Z, twl));
+        // C2R with the pre-twiddle fused into its first stage (wave_c2r),
+        // ping-ponging through prel and Z: Q -- this block's spectrum --
+        // stays intact for the helpers' next near sum
+        const float *y = wave_c2r<LOG2B>(Z, prel, Z, twl);
 #pragma unroll
         for (int i = 0; i < B / 64; ++i) {  // overlap-add (:270-274) + two-stage adds (:439-454)
             const int j = lane + 64 * i;
