@@ -1125,13 +1125,16 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
 
 // The same transforms one segment per wave (64 <= B <= 1024): the twiddle
 // table is staged in LDS once per workgroup, the stages synchronise at wave
-// level, and each wave walks IR_SPW segments.  Same butterflies in the same
-// order as ir_segments_kernel, so the same bits.
+// level, and each wave walks IR_SPW segments, loading the next segment's
+// samples into registers while it transforms the current one (the transform
+// was a dependent load -> FFT -> store chain per segment).  Same butterflies
+// in the same order as ir_segments_kernel, so the same bits.
 // grid (ceil(S / (4 * IR_SPW)), channels); LDS: tw (2B) | 4 x (bufA | bufB)
 constexpr int IR_SPW = 2;
 template <int LOG2B>
 __global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
     constexpr int B = 1 << LOG2B;
+    constexpr int NPL = (B / 2 + 63) / 64;  // packed input points per lane (the upper half is padding)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2 *twl = reinterpret_cast<float2 *>(smem);
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1153,29 +1156,44 @@ __global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
             a.state[c].w &= ~(FLAG_PRE | LA_MASK | SEQ_MASK);  // the stored pre / window used the old response
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     const float *src = a.src + blockIdx.y * a.src_stride;
+    // copy_and_pad (:56-60) of segment i as packed points z[m] = (x[2m], x[2m+1]), m < B/2
+    auto load = [&](int i, float2 (&z)[NPL]) {
+        const long long base = (long long)i * B;
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) {
+            const int m = lane + 64 * u;
+            const long long i0 = base + 2 * m, i1 = i0 + 1;
+            z[u].x = (2 * m < B && i0 < a.len_data) ? src[i0] : 0.f;
+            z[u].y = (2 * m + 1 < B && i1 < a.len_data) ? src[i1] : 0.f;
+        }
+    };
+    const int i0 = (blockIdx.x * 4 + wave) * IR_SPW;
+    float2 cur[NPL], nxt[NPL];
+    if (i0 < a.S && i0 < active) load(i0, cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // (the twiddle table)
     for (int q = 0; q < IR_SPW; ++q) {
-        const int i = (blockIdx.x * 4 + wave) * IR_SPW + q;
+        const int i = i0 + q;
         if (i >= a.S) break;
         float2 *row = a.H + c * rows + (size_t)i * B;
+        if (i + 1 < a.S && i + 1 < active && q + 1 < IR_SPW) load(i + 1, nxt);  // (in flight under this FFT)
         if (i >= active) {  // :210-212
             for (int m = lane; m < B; m += 64) row[m] = make_float2(0.f, 0.f);
             continue;
         }
-        const long long base = (long long)i * B;
-        for (int m = lane; m < B; m += 64) {
-            const long long i0 = base + 2 * m, i1 = base + 2 * m + 1;
-            float2 z;
-            z.x = (2 * m < B && i0 < a.len_data) ? src[i0] : 0.f;
-            z.y = (2 * m + 1 < B && i1 < a.len_data) ? src[i1] : 0.f;
-            bufA[m] = z;
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) {
+            const int m = lane + 64 * u;
+            if (m < B) bufA[m] = m < B / 2 ? cur[u] : make_float2(0.f, 0.f);
         }
+        for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
         wave_sync();
         const float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);
         for (int m = lane; m < B; m += 64) row[m] = real_post<LOG2B, 64>(Z, m, twl);
         wave_sync();  // (the next segment overwrites both buffers)
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) cur[u] = nxt[u];
     }
 }
 

@@ -7,6 +7,11 @@ inputs, HIP events on the launch stream).  Prints one JSON line per config.
   cfg5: CrossfadeConvolver<FFTConvolver>, 512 channels, block 512, IR 96000,
         update() with a fresh IR every 128 blocks (trait init: crossfade over
         response.len() samples, so most updates take the pending path).
+  cfg1: BASELINE configs[0] -- ONE channel, block 256, IR 4096, the CPU path
+        (examples/compare_partitioned.rs:28-53 plumbing: one process() per block,
+        wall clock around the loop): the oracle port on one thread, next to the
+        same single-channel call sequence on the GPU through the host-buffer C ABI
+        (PCIe round trip + launch per 256-sample block: latency, not throughput).
   cfg2u: cfg2 (1024 channels, block 256, IR 48000) with update_device() of
         every channel every 128 blocks (the post-update launches under
         rocprofv3 show whether an IR swap costs the process path anything).
@@ -233,6 +238,31 @@ def main():
         del conv, fresh
         if not a.no_cpu and not a.pmc_inner:
             out[-1]["cpu_baseline"] = cpu_baseline("crossfade", C, B, L, every=128)
+    if "1" in a.configs.split(",") and not a.pmc_inner:
+        B, L, nb = 256, 4096, 4000
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # the CPU path (port of the reference's algorithm)
+
+        secs = oracle.bench("uniform", 1, B, L, nb, 100, 1)
+        ir1 = shard.synth_irs(range(1), L)[0]
+        x1 = shard.synth_dry(range(1), 64, B)[:, 0, :]
+        conv1 = F.FFTConvolver.init(ir1, B, L)
+        for i in range(100):
+            conv1.process(x1[i % 64])
+        t0 = time.perf_counter()
+        for i in range(nb):
+            conv1.process(x1[i % 64])
+        gsec = time.perf_counter() - t0
+        out.append({"config": "cfg1 FFTConvolver, 1 channel, block 256, IR 4096 (CPU path)", "blocks": nb,
+                    "cpu_baseline": {"value": round(B * nb / secs / 1e6, 3), "unit": "MSamples/s", "cores": 1,
+                                     "kind": "port", "us_per_block": round(secs / nb * 1e6, 3),
+                                     "sample": f"oracle/fftconv_oracle.c FFTConvolver, 1 channel x {nb} blocks of "
+                                               f"{B}, one thread (the reference is one instance on one thread)"},
+                    "gpu_host_path": {"value": round(B * nb / gsec / 1e6, 3), "unit": "MSamples/s",
+                                      "us_per_block": round(gsec / nb * 1e6, 3),
+                                      "note": "fftconv_uniform_process per block from Python (H2D + launch + D2H "
+                                              "+ stream sync): one channel is latency-bound on a GPU"}})
+        del conv1
     if "2u" in a.configs.split(","):
         C, B, L = 1024, 256, 48000
         conv = F.FFTConvolver.init(shard.synth_irs(range(C), L), B, L, channels=C)
