@@ -945,6 +945,13 @@ struct CrossfadeCore {
     bool poisoned = false;
     mutable StreamOrder order;
     PinnedStage hstage;  // host responses for the pending path (stored_response)
+    // CrossfadeConvolver<TwoStageFFTConvolver> (the reference is generic over
+    // Convolution, :11,45-49): convolver_a only.  B starts as A's clone and is
+    // never switched to: every swap (:94-105) reaches TwoStageFFTConvolver::
+    // update, todo!() (src/fft_convolver.rs:408-410), before fade_into, so the
+    // crossfader stays Reached(A) and mix() returns A's sample (:244-247).  B
+    // would run the same work on the same state and is never observable.
+    std::unique_ptr<TwoStageCore> ts;
     int check_poisoned() const {
         return poisoned ? fail(FFTCONV_E_DEVICE, "crossfade handle unusable: an earlier process() failed between "
                                                   "its two convolvers' launches")
@@ -996,6 +1003,49 @@ struct CrossfadeCore {
         return FFTCONV_OK;
     }
 
+    // CrossfadeConvolver::<TwoStageFFTConvolver>::new (:19-43), taking
+    // ownership of the (already cloned / freshly initialised) inner convolver
+    int init_new_ts(std::unique_ptr<TwoStageCore> inner, size_t max_response_length, size_t mbs,
+                    size_t crossfade_samples) {
+        device = inner->device;
+        C = inner->C;
+        DeviceGuard g(device);
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        ts = std::move(inner);
+        stored_len = max_response_length;  // (stored_response is never written: no swap can start)
+        stored_stride = stored_len;
+        xf.init(crossfade_samples, std::min(mbs, max_response_length));
+        max_buffer_size = mbs;
+        return buf_a.alloc(C * mbs);
+    }
+
+    int ts_update_unimplemented() const {
+        return fail(FFTCONV_E_UNIMPLEMENTED, "not yet implemented (the swap calls TwoStageFFTConvolver::update, "
+                                             "which is todo!())");
+    }
+
+    // :66-78 over a TwoStageFFTConvolver: convolver_a.process(input, buffer_a)
+    // on max_buffer_size samples, then mix() = A's samples (Reached(A))
+    int process_ts(const float *din, size_t is, float *dout, size_t os, size_t out_len, hipStream_t s) {
+        const size_t m = max_buffer_size;
+        if (m > ts->head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
+        if (m == 0 || C == 0) return FFTCONV_OK;
+        const bool direct = out_len == m;
+        if (int r = ts->process_device(din, is, direct ? dout : buf_a.p, direct ? os : m, m, s)) return r;
+        if (!direct && out_len)
+            HIP_TRY(hipMemcpy2DAsync(dout, os * sizeof(float), buf_a.p, m * sizeof(float), out_len * sizeof(float), C,
+                                     hipMemcpyDeviceToDevice, s));
+        xf.advance(out_len);
+        return FFTCONV_OK;
+    }
+
+    // every piece of the handle's work has finished (incl. a TwoStage inner's
+    // tail convolution on its side stream)
+    int quiesce() const {
+        if (int r = order.drain(stream)) return r;
+        return ts ? ts->quiesce() : FFTCONV_OK;
+    }
+
     bool is_crossfading() const { return xf.approaching; }  // :85-92
 
     // swap (:94-105) from device samples
@@ -1026,6 +1076,7 @@ struct CrossfadeCore {
     // staged in pinned memory and the work enqueued behind the handle's.
     int update_host(const float *src, size_t len, size_t stride) {
         if (int r = check_poisoned()) return r;
+        if (ts) return ts_update_unimplemented();
         DeviceGuard g(device);
         if (int r = order.enter(stream)) return r;
         if (!is_crossfading()) {
@@ -1061,6 +1112,7 @@ struct CrossfadeCore {
     // Convolution::update (:51-64) from device samples, stream-ordered
     int update_device(const float *src, size_t len, size_t stride, hipStream_t s) {
         if (int r = check_poisoned()) return r;
+        if (ts) return ts_update_unimplemented();
         if (!is_crossfading()) {
             UniformCore &t = xf.target == 0 ? *b : *a;
             if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
@@ -1098,6 +1150,7 @@ struct CrossfadeCore {
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t out_len, hipStream_t s) {
         if (int r = check_poisoned()) return r;
         if (out_len > max_buffer_size) return fail(FFTCONV_E_INVALID, "output longer than max_buffer_size (index out of bounds)");
+        if (ts) return process_ts(din, is, dout, os, out_len, s);
         if (!is_crossfading() && response_pending) {                    // :67-70
             if (int r = swap_device(stored.p, stored_stride, stored_len, s)) return r;
             response_pending = false;
@@ -1181,6 +1234,9 @@ struct CrossfadeCore {
 
     int process_host(const float *in, size_t in_len, float *out, size_t out_len) {
         if (in_len < max_buffer_size) return fail(FFTCONV_E_INVALID, "input shorter than max_buffer_size (range end index out of range)");
+        if (ts && in_len > max_buffer_size)  // TwoStage: assert (:414), then output[i] past buffer_a (:441)
+            return fail(FFTCONV_E_INVALID, in_len > ts->head_bs ? "assertion failed: input.len() <= self.head_block_size"
+                                                                : "index out of bounds (input longer than max_buffer_size)");
         if (out_len > max_buffer_size) return fail(FFTCONV_E_INVALID, "output longer than max_buffer_size (index out of bounds)");
         if (C == 0) return FFTCONV_OK;
         DeviceGuard g(device);
@@ -1206,6 +1262,12 @@ struct CrossfadeCore {
         xf = o.xf; response_pending = o.response_pending;
         act[0] = o.act[0]; act[1] = o.act[1]; pair_ok = o.pair_ok; poisoned = o.poisoned;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        if (o.ts) {
+            ts.reset(new (std::nothrow) TwoStageCore());
+            if (!ts) return fail(FFTCONV_E_NOMEM, "out of host memory");
+            if (int r = ts->clone_from(*o.ts)) return r;
+            return buf_a.alloc(o.buf_a.n);
+        }
         a.reset(new (std::nothrow) UniformCore());
         b.reset(new (std::nothrow) UniformCore());
         if (!a || !b) return fail(FFTCONV_E_NOMEM, "out of host memory");
@@ -1556,6 +1618,34 @@ fftconv_crossfade *fftconv_crossfade_new(const fftconv_uniform *convolver, size_
     int r = h->core.init_new(convolver->core, max_response_length, max_buffer_size, crossfade_samples);
     return make_or_null(r, h);
 }
+// CrossfadeConvolver<TwoStageFFTConvolver>: init (:46-49) / new (:19-43)
+fftconv_crossfade *fftconv_crossfade_init_twostage(const float *response, size_t response_len, size_t max_block_size,
+                                                   size_t max_response_length) {
+    return fftconv_crossfade_init_twostage_batch(0, 1, response, response_len, response_len, max_block_size,
+                                                 max_response_length);
+}
+fftconv_crossfade *fftconv_crossfade_init_twostage_batch(int device, size_t channels, const float *responses,
+                                                         size_t response_len, size_t response_stride,
+                                                         size_t max_block_size, size_t max_response_length) {
+    set_error("");
+    std::unique_ptr<TwoStageCore> inner(new (std::nothrow) TwoStageCore());
+    auto *h = new (std::nothrow) fftconv_crossfade();
+    if (!inner || !h) { delete h; set_error("out of host memory"); return nullptr; }
+    int r = inner->init(device, channels, responses, response_len, channels == 1 ? response_len : response_stride,
+                        max_block_size, max_response_length);
+    if (r == FFTCONV_OK) r = h->core.init_new_ts(std::move(inner), response_len, max_block_size, response_len);
+    return make_or_null(r, h);
+}
+fftconv_crossfade *fftconv_crossfade_new_twostage(const fftconv_twostage *convolver, size_t max_response_length,
+                                                  size_t max_buffer_size, size_t crossfade_samples) {
+    if (!convolver) { set_error("null handle"); return nullptr; }
+    std::unique_ptr<TwoStageCore> inner(new (std::nothrow) TwoStageCore());
+    auto *h = new (std::nothrow) fftconv_crossfade();
+    if (!inner || !h) { delete h; set_error("out of host memory"); return nullptr; }
+    int r = inner->clone_from(convolver->core);
+    if (r == FFTCONV_OK) r = h->core.init_new_ts(std::move(inner), max_response_length, max_buffer_size, crossfade_samples);
+    return make_or_null(r, h);
+}
 int fftconv_crossfade_update(fftconv_crossfade *h, const float *response, size_t len) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     return h->core.update_host(response, len, 0);
@@ -1613,7 +1703,7 @@ void fftconv_crossfade_destroy(fftconv_crossfade *h) { delete h; }
 int fftconv_crossfade_synchronize(fftconv_crossfade *h) {
     if (!h) return fail(FFTCONV_E_INVALID, "null handle");
     DeviceGuard g(h->core.device);
-    return h->core.order.drain(h->core.stream);
+    return h->core.quiesce();
 }
 
 }  // extern "C"

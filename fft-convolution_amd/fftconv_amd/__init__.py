@@ -83,6 +83,9 @@ SIGNATURES = {
     "fftconv_crossfade_init": (_vp, [_fp, _sz, _sz, _sz]),
     "fftconv_crossfade_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
     "fftconv_crossfade_new": (_vp, [_vp, _sz, _sz, _sz]),
+    "fftconv_crossfade_init_twostage": (_vp, [_fp, _sz, _sz, _sz]),
+    "fftconv_crossfade_init_twostage_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
+    "fftconv_crossfade_new_twostage": (_vp, [_vp, _sz, _sz, _sz]),
     "fftconv_crossfade_update": (_i, [_vp, _fp, _sz]),
     "fftconv_crossfade_update_batch": (_i, [_vp, _fp, _sz, _sz]),
     "fftconv_crossfade_update_device": (_i, [_vp, _vp, _sz, _sz, _vp]),
@@ -392,24 +395,42 @@ class TwoStageFFTConvolver(_Base):
 
 
 class CrossfadeConvolver(_Base):
-    """CrossfadeConvolver<FFTConvolver>, src/crossfade_convolver.rs:3-105."""
+    """CrossfadeConvolver<T>, src/crossfade_convolver.rs:3-105, for T =
+    FFTConvolver (the default) or TwoStageFFTConvolver (`inner=`, or `new`
+    with a TwoStageFFTConvolver).  Over a TwoStageFFTConvolver every update()
+    reaches its todo!() (src/fft_convolver.rs:408-410) and raises
+    NotImplementedInReference, as the reference panics."""
 
     _prefix = "crossfade"
 
-    def __init__(self, h, channels: int, max_buffer_size: int):
+    def __init__(self, h, channels: int, max_buffer_size: int, inner: type = None):
         super().__init__(h, channels)
         self.max_buffer_size = max_buffer_size
+        self.inner = inner or FFTConvolver
 
     @classmethod
-    def init(cls, response, max_block_size: int, max_response_length: int, *, channels: int = 1, device: int = 0):
+    def init(cls, response, max_block_size: int, max_response_length: int, *, channels: int = 1, device: int = 0,
+             inner: type = None):
+        """Convolution::init (:46-49); `inner` is the T of CrossfadeConvolver<T>."""
         r, n, stride = _responses(response, channels)
-        h = lib().fftconv_crossfade_init_batch(device, channels, _p(r), n, stride, max_block_size, max_response_length)
-        return cls(_handle(h), channels, max_block_size)
+        fn = lib().fftconv_crossfade_init_twostage_batch if inner is TwoStageFFTConvolver \
+            else lib().fftconv_crossfade_init_batch
+        if inner not in (None, FFTConvolver, TwoStageFFTConvolver):
+            raise TypeError("inner must be FFTConvolver or TwoStageFFTConvolver")
+        h = fn(device, channels, _p(r), n, stride, max_block_size, max_response_length)
+        return cls(_handle(h), channels, max_block_size, inner)
 
     @classmethod
-    def new(cls, convolver: FFTConvolver, max_response_length: int, max_buffer_size: int, crossfade_samples: int):
-        h = lib().fftconv_crossfade_new(convolver._h, max_response_length, max_buffer_size, crossfade_samples)
-        return cls(_handle(h), convolver.channels, max_buffer_size)
+    def new(cls, convolver, max_response_length: int, max_buffer_size: int, crossfade_samples: int):
+        """CrossfadeConvolver::new (:19-43); the convolver is cloned."""
+        if isinstance(convolver, TwoStageFFTConvolver):
+            fn = lib().fftconv_crossfade_new_twostage
+        elif isinstance(convolver, FFTConvolver):
+            fn = lib().fftconv_crossfade_new
+        else:
+            raise TypeError("convolver must be an FFTConvolver or a TwoStageFFTConvolver")
+        h = fn(convolver._h, max_response_length, max_buffer_size, crossfade_samples)
+        return cls(_handle(h), convolver.channels, max_buffer_size, type(convolver))
 
     def update(self, response):
         r = _f32(response)
@@ -439,7 +460,7 @@ class CrossfadeConvolver(_Base):
 
     def clone(self):
         return CrossfadeConvolver(_handle(lib().fftconv_crossfade_clone(self._h)), self.channels,
-                                  self.max_buffer_size)
+                                  self.max_buffer_size, self.inner)
 
 
 __all__ = [

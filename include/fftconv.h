@@ -50,7 +50,7 @@ enum {
 
 typedef struct fftconv_uniform fftconv_uniform;     /* FFTConvolver        src/fft_convolver.rs:86-307 */
 typedef struct fftconv_twostage fftconv_twostage;   /* TwoStageFFTConvolver src/fft_convolver.rs:323-512 */
-typedef struct fftconv_crossfade fftconv_crossfade; /* CrossfadeConvolver<FFTConvolver> src/crossfade_convolver.rs:10-105 */
+typedef struct fftconv_crossfade fftconv_crossfade; /* CrossfadeConvolver<FFTConvolver | TwoStageFFTConvolver> src/crossfade_convolver.rs:10-105 */
 
 /* ---- library ----------------------------------------------------------- */
 int fftconv_abi_version(void);
@@ -207,6 +207,20 @@ fftconv_crossfade *fftconv_crossfade_init_batch(int device, size_t channels, con
  * cloned (the reference moves it; the caller keeps ownership of its handle). */
 fftconv_crossfade *fftconv_crossfade_new(const fftconv_uniform *convolver, size_t max_response_length,
                                          size_t max_buffer_size, size_t crossfade_samples);
+/* CrossfadeConvolver<TwoStageFFTConvolver> (the reference's CrossfadeConvolver
+ * is generic over `Convolution`, src/crossfade_convolver.rs:11,45-49): the same
+ * handle type and the same functions below.  Its update() reaches
+ * TwoStageFFTConvolver::update, todo!() (src/fft_convolver.rs:408-410), before
+ * anything changes: FFTCONV_E_UNIMPLEMENTED and the handle is unchanged.
+ * process() needs input_len == max_buffer_size <= the inner head block size
+ * (:412-414 and the head / tail slice bounds). */
+fftconv_crossfade *fftconv_crossfade_init_twostage(const float *response, size_t response_len,
+                                                   size_t max_block_size, size_t max_response_length);
+fftconv_crossfade *fftconv_crossfade_init_twostage_batch(int device, size_t channels, const float *responses,
+                                                         size_t response_len, size_t response_stride,
+                                                         size_t max_block_size, size_t max_response_length);
+fftconv_crossfade *fftconv_crossfade_new_twostage(const fftconv_twostage *convolver, size_t max_response_length,
+                                                  size_t max_buffer_size, size_t crossfade_samples);
 /* src/crossfade_convolver.rs:51-64; same response for every channel. */
 int fftconv_crossfade_update(fftconv_crossfade *h, const float *response, size_t response_len);
 int fftconv_crossfade_update_batch(fftconv_crossfade *h, const float *responses, size_t response_len,

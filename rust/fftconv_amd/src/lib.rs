@@ -74,6 +74,8 @@ gpu_convolver!(GpuTwoStageFFTConvolver, fftconv_twostage, fftconv_twostage_init,
                fftconv_twostage_reset, fftconv_twostage_clone, fftconv_twostage_destroy);
 gpu_convolver!(GpuCrossfadeConvolver, fftconv_crossfade, fftconv_crossfade_init, fftconv_crossfade_update,
                fftconv_crossfade_reset, fftconv_crossfade_clone, fftconv_crossfade_destroy);
+gpu_convolver!(GpuCrossfadeTwoStageConvolver, fftconv_crossfade, fftconv_crossfade_init_twostage,
+               fftconv_crossfade_update, fftconv_crossfade_reset, fftconv_crossfade_clone, fftconv_crossfade_destroy);
 
 /// FFTConvolver (src/fft_convolver.rs:86-307).
 impl Convolution for GpuFFTConvolver {
@@ -143,6 +145,44 @@ impl GpuCrossfadeConvolver {
         let p = unsafe {
             ffi::fftconv_crossfade_new(convolver.h.as_ptr(), max_response_length, max_buffer_size,
                                        crossfade_samples)
+        };
+        Self { h: handle(p) }
+    }
+    /// src/crossfade_convolver.rs:85-92
+    pub fn is_crossfading(&self) -> bool {
+        unsafe { ffi::fftconv_crossfade_is_crossfading(self.h.as_ptr()) != 0 }
+    }
+}
+
+/// CrossfadeConvolver<TwoStageFFTConvolver> (the reference's CrossfadeConvolver
+/// is generic, src/crossfade_convolver.rs:11,45-49).  `update` reaches
+/// TwoStageFFTConvolver::update's `todo!()` through the swap and panics the
+/// same way; `process` needs input.len() == max_buffer_size <= the head block.
+impl Convolution for GpuCrossfadeTwoStageConvolver {
+    fn init(response: &[f32], max_block_size: usize, max_response_length: usize) -> Self {
+        Self::init_raw(response, max_block_size, max_response_length)
+    }
+    fn update(&mut self, response: &[f32]) {
+        self.update_raw(response)
+    }
+    fn reset(&mut self) {
+        self.reset_raw()
+    }
+    fn process(&mut self, input: &[f32], output: &mut [f32]) {
+        check(unsafe {
+            ffi::fftconv_crossfade_process(self.h.as_ptr(), input.as_ptr(), input.len(), output.as_mut_ptr(),
+                                           output.len())
+        })
+    }
+}
+
+impl GpuCrossfadeTwoStageConvolver {
+    /// CrossfadeConvolver::new (src/crossfade_convolver.rs:20-43) around a GPU TwoStageFFTConvolver.
+    pub fn new(convolver: GpuTwoStageFFTConvolver, max_response_length: usize, max_buffer_size: usize,
+               crossfade_samples: usize) -> Self {
+        let p = unsafe {
+            ffi::fftconv_crossfade_new_twostage(convolver.h.as_ptr(), max_response_length, max_buffer_size,
+                                                crossfade_samples)
         };
         Self { h: handle(p) }
     }
