@@ -1478,7 +1478,7 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         args.lag = 0;
         args.la_channels = channels;
         args.la_steps_first = xf3 ? xf_steps_first() : la_steps_first();
-        args.la_probe = xf3 ? 0 : la_probe();
+        args.la_probe = la_probe();
         if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) {
             args.la_all = -1;  // no anchors: every eligible step sums all its rows
             args.la_nfar = args.la_nmid = 0;
@@ -1490,7 +1490,8 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         const int nstep = (channels + nch - 1) / nch;
         if (a.la_mix == 2 && a.job[0].add0) return hipErrorInvalidValue;  // (the fused mix uses the add buffers' LDS)
         const int xwg = a.la_mix == 1 ? LA_XWG : 0;  // A's launch: the mix_value walk workgroups
-        const int nanch = (xf3 ? 2 : 1) * (args.la_nfar + args.la_nmid);
+        const int nanch = xf3 && args.la_steps_first == 2 ? 2 * args.la_nfar + (2 * args.la_nmid + 7) / 8 * 8
+                                                          : (xf3 ? 2 : 1) * (args.la_nfar + args.la_nmid);
         hipLaunchKernelGGL(kern, dim3(nanch + nstep + xwg), dim3(LA_NT), lds, s, args);
         return hipGetLastError();
     }

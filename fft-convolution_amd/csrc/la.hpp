@@ -61,7 +61,18 @@ constexpr int LA_NT = 256;           // threads per workgroup (anchor and step r
 // and the launch is slower: 21.60 vs 18.62 us.  The launch is bound by its
 // bytes in flight, not by the far chain alone; kept as an option.
 constexpr int LA_HW = 0;
-constexpr int LA_NG = LA_HW ? 8 : 4; // far-row groups
+// far-row groups per anchor: 4 (one full-wave laneset each; a far anchor
+// workgroup's four waves), 8 from B = LA_NG8_B on -- two far parts, i.e. two
+// window rows per step, and twice the far workgroups, each walking half the
+// rows.  Measured at cfg5 (r2t, B = 512): the far walks end sooner, but the
+// launch is bound by its bytes, not by the walks' slots: 45.8 vs 41.7 us per
+// step, so the default keeps 4 groups (LA_NG8_B beyond the lookahead range)
+#ifndef FFTCONV_LA_NG8_B
+#define FFTCONV_LA_NG8_B 1024
+#endif
+constexpr int LA_NG8_B = FFTCONV_LA_NG8_B;
+template <int LOG2B>
+__host__ __device__ constexpr int la_ng() { return LA_HW || (1 << LOG2B) >= LA_NG8_B ? 8 : 4; }
 constexpr int LA_CU = 8;             // full-pass chain: rows in flight per lane
 constexpr int LA_OOB = 0x7ffffff0;   // a buffer voffset past every stream's range
 static_assert(LA_DM <= LA_D1 && LA_DM <= 8 && LA_DF <= 32 && LA_DF % LA_JW == 0, "lookahead levels (state word fields)");
@@ -134,10 +145,12 @@ __device__ __forceinline__ int la_mid_j0(int l, int JM) { return min(l * JM, LA_
 // neighbouring groups then read their shared X rows at the same time)
 __host__ __device__ constexpr bool la_asc(int g) { return LA_HW ? false : (g & 1) != 0; }
 // far-row group g of NG: rows [lo, hi) of [DF+1, act)
+template <int LOG2B>
 __device__ __forceinline__ void la_group(int g, int act, int &lo, int &hi) {
+    constexpr int NG = la_ng<LOG2B>();
     const int nf = act - LA_DF - 1;
-    lo = LA_DF + 1 + (g * nf) / LA_NG;
-    hi = LA_DF + 1 + ((g + 1) * nf) / LA_NG;
+    lo = LA_DF + 1 + (g * nf) / NG;
+    hi = LA_DF + 1 + ((g + 1) * nf) / NG;
 }
 // window rows: far P[c][win][j][w] (w < la_W parts), mid P[c][win][j]
 __device__ __forceinline__ float4 *la_pf(const ProcArgs &a, int jb, size_t c, int win, int j, int w, int B) {
@@ -283,9 +296,10 @@ struct LaGeo {
     // window slices, XCD-aligned (see la_anchor_far)
     static constexpr int FW = LA_HW ? 32 : 64;                      // lanes per far laneset
     static constexpr int FS = F < FW ? F : FW, NSL = F / FS, LPF = LA_NT / FS;
-    static constexpr int GPW = LPF < LA_NG ? LPF : LA_NG;
-    static constexpr int WF = LA_NG / GPW;                          // far parts (P rows per step)
-    static_assert(LA_NG % GPW == 0, "far groups must fill whole parts");
+    static constexpr int NG = la_ng<LOG2B>();
+    static constexpr int GPW = LPF < NG ? LPF : NG;
+    static constexpr int WF = NG / GPW;                             // far parts (P rows per step)
+    static_assert(NG % GPW == 0, "far groups must fill whole parts");
     static constexpr int WG_FAR = NSL * WF * (LA_DF / LA_JW);       // workgroups per far anchor
     static constexpr int JM = la_mid_per(LPW);                      // mid window steps per laneset
     static constexpr size_t anchor_bytes = (size_t)(GPW - 1) * LA_JW * FS * 16;
@@ -375,7 +389,7 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
     const int h = r / (NSL * LG::WF);                  // window slice: steps h*JW+1 .. h*JW+JW
     const int g = w * GPW + l;
     int lo, hi;
-    la_group(g, act, lo, hi);
+    la_group<LOG2B>(g, act, lo, hi);
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
     const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
@@ -388,8 +402,8 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
         static_assert(LG::FS * 2 == 64 && LG::WF == 1, "half-wave far lanesets");
         const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
         int lo0, hi0, lo1, hi1;  // the wave's two groups
-        la_group(2 * wv, act, lo0, hi0);
-        la_group(2 * wv + 1, act, lo1, hi1);
+        la_group<LOG2B>(2 * wv, act, lo0, hi0);
+        la_group<LOG2B>(2 * wv + 1, act, lo1, hi1);
         const int nmax = max(hi0 - lo0, hi1 - lo1);
         if (nmax > 0) la_walk_lane<LOG2B, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, nmax, h * LA_JW, cur, act);
     } else if (hi > lo) {
@@ -475,9 +489,15 @@ struct LaStep {
     static constexpr size_t tw_bytes = 12 * (size_t)B;
     static constexpr size_t ch_bytes = 3 * 8 * (size_t)B + 2 * 4 * (size_t)B;
     static constexpr size_t chain_bytes = tw_bytes + NCH * ch_bytes;
-    // the full pass's chain results (mid + NG far groups per channel) alias
-    // the chain buffers (they are consumed before the chains start)
-    static constexpr size_t grp_bytes = (size_t)NCH * (1 + LA_NG) * F * 16;
+    // the full pass's chain results alias the chain buffers (they are
+    // consumed before the chains start): per channel the mid chain and the NG
+    // far groups -- or, where one laneset runs every chain of a channel in
+    // order (LPW == 1), the mid chain and the WF far parts, each folded group
+    // by group as the anchors combine them
+    static constexpr int NG = la_ng<LOG2B>(), WF = LaGeo<LOG2B>::WF;
+    static constexpr bool FOLD = LPW == 1;
+    static constexpr int GSLOTS = 1 + (FOLD ? WF : NG);
+    static constexpr size_t grp_bytes = (size_t)NCH * GSLOTS * F * 16;
     // (+ the XF 3 mix counter after the chain buffers; it may alias the
     // full pass's results, which are consumed before the counter is set)
     static constexpr size_t cnt_off = chain_bytes;
@@ -518,14 +538,15 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     constexpr int B = LS::B, F = LS::F, LPW = LS::LPW, GPW = LG::GPW, WF = LG::WF;
     constexpr int HL = LA_NT - 64 * NCH;
     constexpr int TPL = (NCH * F + HL - 1) / HL;
-    constexpr int NCHAIN = 1 + LA_NG;  // full pass: mid chain + far groups, per channel
+    constexpr int NCHAIN = 1 + LS::NG;  // full pass: mid chain + far groups, per channel
+    constexpr int GS = LS::GSLOTS;      // LDS result slots per channel (LS::FOLD: parts)
     constexpr int ROWB = B * (int)sizeof(float2);
     constexpr float invN = 1.0f / (float)(2 * B);
     constexpr size_t chb = LS::ch_bytes;
     static_assert(NCH == 1 || NCH == 2, "one or two channels per step workgroup");
     float2 *twl = reinterpret_cast<float2 *>(smem);
     auto chan_lds = [&](int k) { return smem + LS::tw_bytes + (size_t)k * chb; };
-    float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][NCHAIN][F], full pass only
+    float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][GS][F], full pass only
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -588,13 +609,21 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                     lo = LA_D1 + 1;
                     hi = LA_DF + 1;
                 } else {
-                    la_group(q - 1, act, lo, hi);
+                    la_group<LOG2B>(q - 1, act, lo, hi);
                 }
                 LaAcc acc;
                 acc.zero();
                 if (q > 0 && la_asc(q - 1)) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
                 else la_chain<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
-                grp[(k * NCHAIN + q) * F + f] = acc.get();
+                if constexpr (LS::FOLD) {
+                    // this thread ran the earlier groups of the part: fold in
+                    // the anchors' order (group 0 of a part, then + each next)
+                    const int w = q == 0 ? -1 : (q - 1) / GPW, qq = (q - 1) % GPW;
+                    float4 *slot = &grp[(k * GS + 1 + w) * F + f];
+                    *slot = (q == 0 || qq == 0) ? acc.get() : vadd(*slot, acc.get());
+                } else {
+                    grp[(k * GS + q) * F + f] = acc.get();
+                }
             }
         }
         __syncthreads();
@@ -603,14 +632,19 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             for (int t = 0; t < TPL; ++t) {
                 int k, f;
                 if (!task(t, k, f)) continue;
-                if (fullM(k)) Mreg[t] = grp[(k * NCHAIN) * F + f];
+                if (fullM(k)) Mreg[t] = grp[(k * GS) * F + f];
                 if (fullF(k)) {
                     float4 A;
 #pragma unroll
                     for (int w = 0; w < WF; ++w) {
-                        float4 pw = grp[(k * NCHAIN + 1 + w * GPW) * F + f];
+                        float4 pw;
+                        if constexpr (LS::FOLD) {
+                            pw = grp[(k * GS + 1 + w) * F + f];
+                        } else {
+                            pw = grp[(k * GS + 1 + w * GPW) * F + f];
 #pragma unroll
-                        for (int qq = 1; qq < GPW; ++qq) pw = vadd(pw, grp[(k * NCHAIN + 1 + w * GPW + qq) * F + f]);
+                            for (int qq = 1; qq < GPW; ++qq) pw = vadd(pw, grp[(k * GS + 1 + w * GPW + qq) * F + f]);
+                        }
                         A = w == 0 ? pw : vadd(A, pw);
                     }
                     Freg[t] = A;
@@ -986,6 +1020,26 @@ __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsign
     for (int j = threadIdx.x; j < m.n; j += LA_NT) mt[j] = mix_selector(m, j, t);
 }
 
+// XF 3 grid order (ProcArgs::la_steps_first) -> the block's index in the
+// logical order [far A | far B | mid A | mid B | steps], or -1 (padding):
+//   0: logical order; 1: the channels' step workgroups lead the grid (the
+//   latency-critical chains get the CUs first, the anchors fill in);
+//   2: steps, then the mid anchors (padded to a multiple of 8 blocks), then the
+//   far anchors -- the mid anchors start with the launch instead of waiting
+//   for the far walks' slots.  The far anchors keep their XCD placement when
+//   the channel count is a multiple of 8 (nf is one).
+__device__ __forceinline__ int la_xf3_block(const ProcArgs &a) {
+    const int nf = a.la_nfar, nm = a.la_nmid;
+    int b = (int)blockIdx.x;
+    if (a.la_steps_first == 0) return b;
+    if (b < a.la_channels) return b + 2 * (nf + nm);
+    b -= a.la_channels;
+    if (a.la_steps_first == 1) return b;
+    const int mp = (2 * nm + 7) / 8 * 8;
+    if (b < mp) return b < 2 * nm ? 2 * nf + b : -1;
+    return b - mp;
+}
+
 // XF: crossfade role of the launch (ProcArgs::la_mix): 0 none; 1 = A's launch,
 // whose first workgroup also writes the gains of this call's mix_value walk to mix_tab;
 // 2 = B's launch, whose steps mix A's block with their own
@@ -995,19 +1049,21 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
     constexpr int NCH = LS::NCH;
     if constexpr (XF == 3) {
         const int nf = a.la_nfar, nm = a.la_nmid;
-        // (la_steps_first: the channels' step workgroups lead the grid -- the
-        // latency-critical chains get the CUs first, the anchors fill in)
-        int b = (int)blockIdx.x;
-        if (a.la_steps_first) b = b < a.la_channels ? b + 2 * (nf + nm) : b - a.la_channels;
+        const int b = la_xf3_block(a);
+        if (b < 0) return;
+        // (timing / traffic probes, results wrong: 1 steps only, 2 anchors
+        // only, 3 far anchors only, 4 mid anchors only)
+        const int pr = a.la_probe;
         if (b < 2 * nf) {  // (nf is a multiple of 8: B's far anchors keep the XCD placement)
-            la_anchor_far<LOG2B, NTL>(a, b >= nf ? 1 : 0, b >= nf ? b - nf : b, smem);
+            if (pr != 1 && pr != 4) la_anchor_far<LOG2B, NTL>(a, b >= nf ? 1 : 0, b >= nf ? b - nf : b, smem);
             return;
         }
         if (b < 2 * (nf + nm)) {
             const int bm = b - 2 * nf;
-            la_anchor_mid<LOG2B, NTL>(a, bm >= nm ? 1 : 0, bm >= nm ? bm - nm : bm);
+            if (pr != 1 && pr != 3) la_anchor_mid<LOG2B, NTL>(a, bm >= nm ? 1 : 0, bm >= nm ? bm - nm : bm);
             return;
         }
+        if (pr >= 2 && pr <= 4) return;
         const int c = b - 2 * (nf + nm);
         if (c >= a.la_channels) return;
         const int4 va = a.job[0].state[c], vb = a.job[1].state[c];
@@ -1071,9 +1127,8 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
 template <int XF>
 __device__ __forceinline__ int la_role(const ProcArgs &a) {
     if (XF == 3) {
-        int b = (int)blockIdx.x;
-        if (a.la_steps_first) b = b < a.la_channels ? b + 2 * (a.la_nfar + a.la_nmid) : b - a.la_channels;
-        return b < 2 * a.la_nfar ? 0 : (b < 2 * (a.la_nfar + a.la_nmid) ? 1 : 2);
+        const int b = la_xf3_block(a);
+        return b < 0 ? 5 : b < 2 * a.la_nfar ? 0 : (b < 2 * (a.la_nfar + a.la_nmid) ? 1 : 2);
     }
     if (XF == 1 && blockIdx.x < LA_XWG) return 4;  // mix walk
     const int nanchor = a.la_nfar + a.la_nmid;

@@ -6,7 +6,7 @@ import sys
 
 import numpy as np
 
-ROLES = {0: "far", 1: "mid", 2: "step", 4: "mixwalk"}
+ROLES = {0: "far", 1: "mid", 2: "step", 4: "mixwalk", 5: "pad"}
 
 
 def load(path):
