@@ -1123,31 +1123,50 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
     for (int m = tid; m < B; m += NT) row[m] = real_post<LOG2B, NT>(Z, m, a.tw);
 }
 
-// The same transforms one segment per wave (64 <= B <= 1024): the twiddle
-// table is staged in LDS once per workgroup, the stages synchronise at wave
-// level, and each wave walks IR_SPW segments, loading the next segment's
-// samples into registers while it transforms the current one (the transform
-// was a dependent load -> FFT -> store chain per segment).  Same butterflies
-// in the same order as ir_segments_kernel, so the same bits.
-// grid (ceil(S / (4 * IR_SPW)), channels); LDS: tw (2B) | 4 x (bufA | bufB)
+// The same transforms one segment per wave (64 <= B <= 1024), each wave
+// walking IR_SPW segments and loading the next segment's samples into
+// registers while it transforms the current one (the transform was a
+// dependent load -> FFT -> store chain per segment).  For B >= 128 (M = B
+// complex points, the upper half the zero padding):
+//  * stage 0 runs in registers from the loaded samples (wave_stage0_padded:
+//    two of a butterfly's four inputs are padding), so neither the samples
+//    nor the padding go through LDS;
+//  * the middle stages read the per-stage twiddle table (TwStaged: gathered
+//    once per workgroup, consecutive entries per stage -- the full table's
+//    strided reads were the kernel's LDS bank conflicts);
+//  * the last stage and realfft's post-twiddle run in registers with the
+//    mirror bin fetched by __shfl (wave_r2c_post), straight to HBM.
+// Same butterflies and twiddle values in the same order as
+// ir_segments_kernel, so the same bits.
+//  * B >= 128: the middle stages run in place (wave_stages_inplace), so a
+//    wave needs one B-point buffer and a workgroup runs IR_NW = 8 waves --
+//    twice the segment loads in flight per CU of the ping-pong layout.
+// grid (ceil(S / (NW * IR_SPW)), channels); LDS: tw (2B) | NW x bufA (| bufB: B < 128)
 constexpr int IR_SPW = 2;
 template <int LOG2B>
-__global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
+constexpr int ir_nw() { return LOG2B >= 7 ? 8 : 4; }
+template <int LOG2B>
+constexpr size_t ir_wave_lds() { return (size_t)(2 + ir_nw<LOG2B>() * (LOG2B >= 7 ? 1 : 2)) * (1 << LOG2B) * sizeof(float2); }
+template <int LOG2B>
+__global__ __launch_bounds__(64 * ir_nw<LOG2B>()) void ir_segments_wave_kernel(IrArgs a) {
     constexpr int B = 1 << LOG2B;
-    constexpr int NPL = (B / 2 + 63) / 64;  // packed input points per lane (the upper half is padding)
+    constexpr bool REG = LOG2B >= 7;                        // register stage 0 / __shfl last stage
+    constexpr int NW = ir_nw<LOG2B>(), NT = 64 * NW;
+    constexpr int NPL = REG ? stage0_per_lane<LOG2B>() : (B / 2 + 63) / 64;  // per lane: butterflies / points
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2 *twl = reinterpret_cast<float2 *>(smem);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    float2 *bufA = twl + 2 * B + (size_t)wave * 2 * B;
+    float2 *bufA = twl + 2 * B + (size_t)wave * (REG ? 1 : 2) * B;
     float2 *bufB = bufA + B;
     const size_t c = a.chan0 + blockIdx.y;
     const size_t rows = (size_t)a.S * B;
     const long long active = (a.len_active + B - 1) / B;
-    dma_16b<256>(twl, a.tw, 2 * B * (int)sizeof(float2));
+    if constexpr (REG) tws_build<LOG2B, NT>(twl, a.tw, tid);
+    else dma_16b<NT>(twl, a.tw, 2 * B * (int)sizeof(float2));
     if (a.update_state && blockIdx.x == 0) {
         // update(): zero overlap / pre_multiplied / conv, set active (:185-190)
-        for (int j = tid; j < B; j += 256) {
+        for (int j = tid; j < B; j += NT) {
             a.overlap[c * B + j] = 0.f;
             a.pre[c * B + j] = make_float2(0.f, 0.f);
         }
@@ -1158,42 +1177,65 @@ __global__ __launch_bounds__(256) void ir_segments_wave_kernel(IrArgs a) {
     }
     const float *src = a.src + blockIdx.y * a.src_stride;
     // copy_and_pad (:56-60) of segment i as packed points z[m] = (x[2m], x[2m+1]), m < B/2
-    auto load = [&](int i, float2 (&z)[NPL]) {
+    auto point = [&](long long base, int m) {
+        const long long i0 = base + 2 * m, i1 = i0 + 1;
+        float2 z;
+        z.x = (2 * m < B && i0 < a.len_data) ? src[i0] : 0.f;
+        z.y = (2 * m + 1 < B && i1 < a.len_data) ? src[i1] : 0.f;
+        return z;
+    };
+    // REG: lo[t] = z[j], hi[t] = z[j + B/4] for butterflies j = lane + 64 t < B/4;
+    // else lo[u] = z[lane + 64 u]
+    auto load = [&](int i, float2 (&lo)[NPL], float2 (&hi)[NPL]) {
         const long long base = (long long)i * B;
 #pragma unroll
         for (int u = 0; u < NPL; ++u) {
             const int m = lane + 64 * u;
-            const long long i0 = base + 2 * m, i1 = i0 + 1;
-            z[u].x = (2 * m < B && i0 < a.len_data) ? src[i0] : 0.f;
-            z[u].y = (2 * m + 1 < B && i1 < a.len_data) ? src[i1] : 0.f;
+            if constexpr (REG) {
+                if (m < B / 4) {
+                    lo[u] = point(base, m);
+                    hi[u] = point(base, m + B / 4);
+                }
+            } else {
+                lo[u] = point(base, m);
+            }
         }
     };
-    const int i0 = (blockIdx.x * 4 + wave) * IR_SPW;
-    float2 cur[NPL], nxt[NPL];
-    if (i0 < a.S && i0 < active) load(i0, cur);
+    const int i0 = (blockIdx.x * NW + wave) * IR_SPW;
+    float2 cur[NPL], curh[NPL], nxt[NPL], nxth[NPL];
+    if (i0 < a.S && i0 < active) load(i0, cur, curh);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // (the twiddle table)
     for (int q = 0; q < IR_SPW; ++q) {
         const int i = i0 + q;
         if (i >= a.S) break;
         float2 *row = a.H + c * rows + (size_t)i * B;
-        if (i + 1 < a.S && i + 1 < active && q + 1 < IR_SPW) load(i + 1, nxt);  // (in flight under this FFT)
+        if (i + 1 < a.S && i + 1 < active && q + 1 < IR_SPW) load(i + 1, nxt, nxth);  // (in flight under this FFT)
         if (i >= active) {  // :210-212
             for (int m = lane; m < B; m += 64) row[m] = make_float2(0.f, 0.f);
             continue;
         }
+        if constexpr (REG) {
+            wave_stage0_padded<LOG2B>(cur, curh, bufA);
+            wave_sync();
+            wave_r2c_post<LOG2B, 1, TwStaged<LOG2B>, true>(bufA, nullptr, TwStaged<LOG2B>{twl}, nullptr, row);
+        } else {
 #pragma unroll
-        for (int u = 0; u < NPL; ++u) {
-            const int m = lane + 64 * u;
-            if (m < B) bufA[m] = m < B / 2 ? cur[u] : make_float2(0.f, 0.f);
+            for (int u = 0; u < NPL; ++u) {
+                const int m = lane + 64 * u;
+                if (m < B) bufA[m] = m < B / 2 ? cur[u] : make_float2(0.f, 0.f);
+            }
+            for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
+            wave_sync();
+            const float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);
+            for (int m = lane; m < B; m += 64) row[m] = real_post<LOG2B, 64>(Z, m, twl);
         }
-        for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
-        wave_sync();
-        const float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);
-        for (int m = lane; m < B; m += 64) row[m] = real_post<LOG2B, 64>(Z, m, twl);
         wave_sync();  // (the next segment overwrites both buffers)
 #pragma unroll
-        for (int u = 0; u < NPL; ++u) cur[u] = nxt[u];
+        for (int u = 0; u < NPL; ++u) {
+            cur[u] = nxt[u];
+            if constexpr (REG) curh[u] = nxth[u];
+        }
     }
 }
 
@@ -1364,13 +1406,14 @@ template <int LOG2B>
 static hipError_t launch_ir_t(const IrArgs &a, int channels, hipStream_t s) {
     if constexpr (LOG2B >= 6 && LOG2B <= 10) {
         if (g_variant == VARIANT_AUTO || !(g_variant & VARIANT_IRBLOCK)) {
-            constexpr size_t lds = 10 * (size_t)(1 << LOG2B) * sizeof(float2);  // tw + 4 waves x 2 buffers
+            constexpr size_t lds = ir_wave_lds<LOG2B>();
+            constexpr int NW = ir_nw<LOG2B>();
             auto kern = ir_segments_wave_kernel<LOG2B>;
             if (lds > 64 * 1024) {
                 hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 if (e != hipSuccess) return e;
             }
-            hipLaunchKernelGGL(kern, dim3((a.S + 4 * IR_SPW - 1) / (4 * IR_SPW), channels), dim3(256), lds, s, a);
+            hipLaunchKernelGGL(kern, dim3((a.S + NW * IR_SPW - 1) / (NW * IR_SPW), channels), dim3(64 * NW), lds, s, a);
             return hipGetLastError();
         }
     }

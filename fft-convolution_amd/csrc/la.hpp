@@ -504,6 +504,17 @@ struct LaStep {
     static constexpr size_t bytes = chain_bytes + 16 > grp_bytes ? chain_bytes + 16 : grp_bytes;
 };
 
+// A register value the compiler must treat as produced here.  The pre's
+// "full-pass result (registers) or window row (HBM)" would otherwise be folded
+// into ONE load through a selected pointer, which moves Mreg / Freg to scratch:
+// a 32 B/lane scratch zero-fill in every step workgroup of every launch (4 MB
+// of writes per cfg2 launch, left dirty at the kernel boundary) and flat loads
+// for every window row.
+__device__ __forceinline__ float4 la_opaque(float4 v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    return v;
+}
+
 // launch timeline phase stamp k (0..3) of this wave (FFTCONV_LA_TRACE)
 __device__ __forceinline__ void la_stamp(const ProcArgs &a, int k) {
     if (a.la_trace && (threadIdx.x & 63) == 0) {
@@ -731,12 +742,12 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             }
             float4 M, A;
             if (fullM(k)) {
-                M = Mreg[t];
+                M = la_opaque(Mreg[t]);
             } else {
                 M = la_pm(a, JB(k), c, (flags & FLAG_PWINM) ? 1 : 0, la_jm(flags), B)[f];
             }
             if (fullF(k)) {
-                A = Freg[t];
+                A = la_opaque(Freg[t]);
             } else {
                 const float4 *P0 = la_pf(a, JB(k), c, (flags & FLAG_PWIN) ? 1 : 0, la_jf(flags), 0, B);
                 A = P0[f];
