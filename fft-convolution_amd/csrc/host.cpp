@@ -611,6 +611,15 @@ struct TwoStageCore {
     hipStream_t side = nullptr;
     hipEvent_t ev_main = nullptr, ev_tail = nullptr;
     bool tail_in_flight = false;
+    // tail0 deferred to the end of its period (launch_tail0_flush): the
+    // aligned calls' blocks [t0_off, t0_off + t0_n * head_bs) of tail_input
+    // still to be convolved by tail_convolver0 (FFTCONV_TAIL0_DEFER=0: off)
+    bool t0_defer = false;
+    mutable size_t t0_off = 0, t0_n = 0;
+    size_t t0_nmax = 0;
+    DevPtr<float2> t0_xs;
+    DevPtr<float> t0_ys;
+    DevPtr<int> t0_err;
     Scratch scratch;
     mutable StreamOrder order;
 
@@ -675,6 +684,30 @@ struct TwoStageCore {
         tail_output0 = out0.p; tail_precalculated0 = pre0.p;
         tail_output = out1.p; tail_precalculated = pre1.p;
         tin_idx = 0;
+        static const bool defer = [] { const char *e = getenv("FFTCONV_TAIL0_DEFER"); return !e || atoi(e) != 0; }();
+        t0_defer = defer && tail0 && tail0->B == head_bs && tail0_defer_supported(tail0->log2b);
+        if (t0_defer) {
+            t0_nmax = T / head_bs;
+            if (int r = t0_xs.alloc(C * t0_nmax * head_bs)) return r;
+            if (int r = t0_ys.alloc(C * t0_nmax * 2 * head_bs)) return r;
+            if (int r = t0_err.alloc(C)) return r;
+            HIP_TRY(hipMemsetAsync(t0_err.p, 0, t0_err.bytes(), stream));
+        }
+        t0_off = t0_n = 0;
+        return FFTCONV_OK;
+    }
+
+    // tail_convolver0.process (:464-472) of the deferred blocks, in one pass
+    int flush_t0(hipStream_t s) const {
+        if (t0_n == 0) return FFTCONV_OK;
+        Tail0Args a{};
+        a.pa.job[0] = tail0->job(tail_input() + t0_off, T, tail_output0 + t0_off, T, head_bs);
+        a.pa.tw = tail0->tw.p;
+        a.pa.njobs = 1;
+        a.xs = t0_xs.p; a.ys = t0_ys.p; a.err = t0_err.p;
+        a.n = (int)t0_n; a.nmax = (int)t0_nmax;
+        t0_n = 0;
+        HIP_TRY(launch_tail0_flush(tail0->log2b, a, (int)C, s));
         return FFTCONV_OK;
     }
 
@@ -733,6 +766,7 @@ struct TwoStageCore {
     // fill reached T (:464-491): swap the tail0 buffers, swap the tail buffers,
     // and start the tail convolution of this period on the side stream.
     int end_of_period(hipStream_t s) {
+        if (int r = flush_t0(s)) return r;  // (tail_output0 is complete before the swap)
         std::swap(tail_precalculated0, tail_output0);                         // :473-475
         std::swap(tail_precalculated, tail_output);                           // :483
         // work after this point reads the swapped-in tail_precalculated: it is
@@ -766,7 +800,10 @@ struct TwoStageCore {
             a.job[0].tin = tail_input() + tail_input_fill;                     // :459-461
             a.job[0].tin_stride = (long long)T;
             a.njobs = 1;
-            if (tail0) {                                                        // :464-472
+            if (tail0 && t0_defer) {                                            // :464-472, deferred
+                if (t0_n == 0) t0_off = tail_input_fill;
+                ++t0_n;
+            } else if (tail0) {                                                 // :464-472
                 a.job[1] = tail0->job(din, is, tail_output0 + tail_input_fill, T, head_bs);
                 a.njobs = 2;
             }
@@ -779,6 +816,7 @@ struct TwoStageCore {
             }
             return FFTCONV_OK;
         }
+        if (int r = flush_t0(s)) return r;  // (the sub-chunk loop runs tail0 per block)
         if (int r = head->process_device(din, is, dout, os, len, s)) return r;   // :417
         size_t processed = 0;
         while (processed < len) {                                                 // :427
@@ -830,6 +868,7 @@ struct TwoStageCore {
         tail_input_fill = 0;
         precalculated_pos = 0;
         tail_in_flight = false;
+        t0_n = 0;  // (the deferred blocks' state is reset with everything else)
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -837,6 +876,10 @@ struct TwoStageCore {
     int clone_from(const TwoStageCore &o) {
         DeviceGuard g(o.device);
         if (int r = o.quiesce()) return r;
+        if (o.t0_n) {  // the source's deferred tail0 blocks first: the copy starts with none
+            if (int r = o.flush_t0(o.stream)) return r;
+            HIP_TRY(hipStreamSynchronize(o.stream));
+        }
         device = o.device; C = o.C; head_bs = o.head_bs; T = o.T;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         auto cl = [&](std::unique_ptr<UniformCore> &dst, const std::unique_ptr<UniformCore> &src) -> int {

@@ -1340,6 +1340,156 @@ constexpr int kNT = 256;
 // blocks get more lanes so each owns <= 4 slots (no spills at 4 waves/SIMD)
 constexpr int proc_nt(int log2b) { return log2b <= 10 ? 256 : (log2b == 11 ? 512 : 1024); }
 
+// ---------------------------------------------------------------------------
+// Two-stage tail0 deferred to the end of its period (Tail0Args, kernels.hpp).
+// TwoStageFFTConvolver::process runs tail_convolver0 on every head block
+// (src/fft_convolver.rs:464-472), but tail_output0 is first read after the
+// period's swap (:473-475).  So the period's blocks are convolved together:
+// one pass over tail0's IR rows and FDL serves all of them, instead of one
+// pass per block (cfg3: 64 passes of 64 rows per period).  The state
+// (FDL, overlap, current) is committed exactly as the per-block calls leave
+// it.
+// ---------------------------------------------------------------------------
+// (1) copy_and_pad + Fft::forward (:229-241) of pending block k of channel c
+// -- the step's own transform -- into xs[c][k]
+template <int LOG2B>
+__global__ __launch_bounds__(64) void tail0_r2c_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *bufA = reinterpret_cast<float2 *>(smem), *bufB = bufA + B, *twl = bufB + B;
+    const ProcJob &J = t.pa.job[0];
+    const size_t c = blockIdx.x;
+    const int k = blockIdx.y, lane = threadIdx.x;
+    dma_f32<64>(reinterpret_cast<float *>(bufA), J.in + c * J.in_stride + (size_t)k * B, B);  // packed z[0..B/2)
+    for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);              // the padding half
+    dma_16b<64>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);
+    float2 *xr = t.xs + ((size_t)c * t.nmax + k) * B;
+    for (int m = lane; m < B; m += 64) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
+}
+
+// (2) conv_k = sum_{i=1}^{act-1} H[i] (.) X_{k-i} + H[0] (.) X_k (:244-261,
+// the reference's row order) for a tile of KT blocks of one channel (thread
+// = block x slot; X_{k-i} is pending block k-i, or for i > k the FDL row
+// (cur0 + i - k) % act of the previous period, untouched so far), then the
+// C2R of each block (:264, one wave per block; the 1/N is applied by (3))
+template <int LOG2B>
+__global__ __launch_bounds__(256) void tail0_mac_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B, F = B / 2, KT = 256 / F;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *twl = reinterpret_cast<float2 *>(smem), *zs = twl + 2 * B, *qs = zs + KT * B;
+    const ProcJob &J = t.pa.job[0];
+    const size_t c = blockIdx.x;
+    const int tid = threadIdx.x, kk = tid / F, f = tid % F;
+    const int k = blockIdx.y * KT + kk;
+    dma_16b<256>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
+    const int4 st = J.state[c];
+    const int cur0 = st.x, act = st.y;
+    const size_t rows = (size_t)J.S * B;
+    const float4 *H = reinterpret_cast<const float4 *>(J.H + c * rows);
+    const float4 *X = reinterpret_cast<const float4 *>(J.X + c * rows);
+    const float4 *xs = reinterpret_cast<const float4 *>(t.xs + (size_t)c * t.nmax * B);
+    if (k < t.n) {
+        Acc2 acc;
+        acc.zero();
+        for (int i = 1; i < act; ++i) {
+            const int m = k - i;
+            int r = cur0 + i - k;
+            if (r >= act) r -= act;
+            const float4 *xp = m >= 0 ? xs + (size_t)m * F : X + (size_t)r * F;
+            acc.mac(H[(size_t)i * F + f], xp[f]);
+        }
+        const float4 cv = slot_mac(acc.get(f), xs[(size_t)k * F + f], H[f], f);
+        reinterpret_cast<float4 *>(zs + kk * B)[f] = cv;
+        if (f == 0 && !slot0_finite(cv)) t.err[c] = 1;  // realfft's C2R error (:264-267)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63;
+    float2 *q = qs + wave * B;
+    for (int b = wave; b < KT; b += 4) {
+        const int kb = blockIdx.y * KT + b;
+        if (kb >= t.n) break;
+        float2 *Z = zs + b * B;
+        for (int m = lane; m < B; m += 64) q[m] = real_pre<LOG2B, 64>(Z, m, twl);
+        wave_sync();
+        const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(q, Z, twl));
+        float *yr = t.ys + ((size_t)c * t.nmax + kb) * 2 * B;
+        for (int j = lane; j < 2 * B; j += 64) yr[j] = y[j];
+        wave_sync();
+    }
+}
+
+// (3) per channel: overlap-add (:270-274) and overlap save (:283-284) over
+// the pending blocks, the FDL rows (block k at (cur0 - k) % act; the last
+// act blocks stay), current and the flags -- or, if any block's C2R failed,
+// tail_convolver0.process block by block (:464-472) from the untouched state
+// by the generic step, so errors leave exactly the reference's state
+template <int LOG2B>
+__device__ __attribute__((noinline)) void tail0_replay(const Tail0Args *tp, size_t c, unsigned char *smem) {
+    constexpr int B = 1 << LOG2B, NT = proc_nt(LOG2B);
+    const Tail0Args &t = *tp;
+    const ProcJob &J = t.pa.job[0];
+    for (int k = 0; k < t.n; ++k) {
+        ProcJob Jk = J;
+        Jk.in = J.in + (size_t)k * B;
+        Jk.out = J.out + (size_t)k * B;
+        Jk.n = B;
+        __syncthreads();  // the previous block's state word is stored
+        const int4 st = J.state[c];
+        process_job<LOG2B, NT, false, false>(t.pa, Jk, c, st, smem);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) t.err[c] = 0;
+}
+template <int LOG2B>
+__global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_finish_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B, NT = proc_nt(LOG2B);
+    constexpr float invN = 1.0f / (float)(2 * B);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ProcJob &J = t.pa.job[0];
+    const size_t c = blockIdx.x;
+    const int tid = threadIdx.x, n = t.n;
+    if (t.err[c]) {  // (the arguments by their kernarg address: no private copy)
+        tail0_replay<LOG2B>((const Tail0Args *)__builtin_amdgcn_kernarg_segment_ptr(), c, smem);
+        return;
+    }
+    const int4 st = J.state[c];
+    const int cur0 = st.x, act = st.y;
+    const float *ys = t.ys + (size_t)c * t.nmax * 2 * B;
+    float *outc = J.out + c * J.out_stride;
+    float *ovc = J.overlap + c * B;
+    for (int idx = tid; idx < n * B; idx += NT) {
+        const int k = idx >> LOG2B, j = idx & (B - 1);
+        const float ov = k == 0 ? ovc[j] : ys[(size_t)(k - 1) * 2 * B + B + j] * invN;
+        outc[idx] = ys[(size_t)k * 2 * B + j] * invN + ov;
+    }
+    __syncthreads();  // every read of the old overlap is done
+    for (int j = tid; j < B; j += NT) ovc[j] = ys[(size_t)(n - 1) * 2 * B + B + j] * invN;
+    if (st.w & FLAG_INBUF) {  // a completed block empties the input buffer (:280)
+        float *ibc = J.inbuf + c * B;
+        for (int j = tid; j < B; j += NT) ibc[j] = 0.f;
+    }
+    const size_t rows = (size_t)J.S * B;
+    float2 *Xc = J.X + c * rows;
+    const float2 *xs = t.xs + (size_t)c * t.nmax * B;
+    const int k0 = n > act ? n - act : 0;
+    for (int idx = tid; idx < (n - k0) * B; idx += NT) {
+        const int k = k0 + (idx >> LOG2B), m = idx & (B - 1);
+        int r = (cur0 - k) % act;
+        if (r < 0) r += act;
+        Xc[(size_t)r * B + m] = xs[(size_t)k * B + m];
+    }
+    if (tid == 0) {
+        int cur = (cur0 - n) % act;
+        if (cur < 0) cur += act;
+        const int flags = (st.w & ~(FLAG_PRE | FLAG_INBUF)) ^ ((n & 1) ? FLAG_REV : 0);
+        J.state[c] = make_int4(cur, act, 0, la_clear(flags, t.pa));
+    }
+}
+
 static int g_variant = VARIANT_AUTO;
 static int g_lag = -1;
 
@@ -1400,6 +1550,37 @@ static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t 
     }
     hipLaunchKernelGGL(kern, dim3(channels, a.njobs), dim3(PNT), Gm::lds_bytes, s, args);
     return hipGetLastError();
+}
+
+template <int LOG2B>
+static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s) {
+    if constexpr (LOG2B >= 6 && LOG2B <= 9) {
+        constexpr int B = 1 << LOG2B, KT = 256 / (B / 2), NT = proc_nt(LOG2B);
+        if (a.n <= 0 || a.n > a.nmax) return hipErrorInvalidValue;
+        Tail0Args t = a;
+        const int var = pick_variant(a.pa, channels, LOG2B);
+        t.pa.pipe = (var & VARIANT_NOPIPE) ? 0 : 1;  // (the replay path's generic step)
+        t.pa.lag = pipeline_lag(LOG2B);
+        hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
+        hipLaunchKernelGGL(tail0_mac_kernel<LOG2B>, dim3(channels, (a.n + KT - 1) / KT), dim3(256),
+                           (size_t)(6 + KT) * B * sizeof(float2), s, t);
+        constexpr size_t fin_lds = Geo<LOG2B, NT>::lds_bytes;  // (the replay path's generic step)
+        hipLaunchKernelGGL(tail0_finish_kernel<LOG2B>, dim3(channels), dim3(NT), fin_lds, s, t);
+        return hipGetLastError();
+    } else {
+        return hipErrorNotSupported;
+    }
+}
+bool tail0_defer_supported(int log2b) { return log2b >= 6 && log2b <= 9; }
+hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    switch (log2b) {
+        case 6: return launch_tail0_t<6>(a, channels, s);
+        case 7: return launch_tail0_t<7>(a, channels, s);
+        case 8: return launch_tail0_t<8>(a, channels, s);
+        case 9: return launch_tail0_t<9>(a, channels, s);
+        default: return hipErrorNotSupported;
+    }
 }
 
 template <int LOG2B>

@@ -198,6 +198,24 @@ hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStre
 hipError_t launch_la_rebuild(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 bool la_full_variant();  // VARIANT_LAFULL: lookahead launches without anchors
 
+// Two-stage tail0 deferred to the end of its period (src/fft_convolver.rs
+// :464-475: tail_output0 is first read after the period's swap).  pa.job[0]
+// is tail0's job with in = tail_input + off, out = tail_output0 + off (both
+// stride T); the n pending blocks of every channel are transformed, summed
+// against one pass of tail0's IR rows and FDL, inverted, and committed --
+// or, for a channel whose C2R fails on any block (realfft's error path),
+// replayed block by block by the generic step from the untouched state.
+struct Tail0Args {
+    ProcArgs pa;
+    float2 *xs;            // [C][nmax][B]: spectra of the pending blocks
+    float *ys;             // [C][nmax][2B]: their C2R outputs (not yet scaled)
+    int *err;              // [C]: some pending block's C2R fails
+    int n;                 // pending blocks
+    int nmax;              // row pitch of xs / ys in blocks
+};
+bool tail0_defer_supported(int log2b);
+hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s);
+
 constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)
 
 }  // namespace fftconv

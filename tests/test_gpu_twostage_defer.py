@@ -1,0 +1,105 @@
+"""Two-stage tail0 deferred to the end of its period (csrc/kernels.hip
+tail0_*_kernel; TwoStageFFTConvolver::process, src/fft_convolver.rs:464-475:
+tail_output0 is first read after the period's swap, so the period's head
+blocks are convolved by tail_convolver0 in one pass).  Checked against the
+oracle through the cases that break the deferral: an unaligned call in the
+middle of a period (flush, then the reference's sub-chunk loop), clone and
+reset with blocks pending, and a non-finite block (realfft's C2R error) in a
+pending set, which replays tail0 block by block from the untouched state.
+Tolerance: REL_TOL (tests/common.py)."""
+import numpy as np
+import pytest
+
+from common import assert_close, ir, white
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(conv, ref, rng, chunks, nan_at=(), channels=1):
+    """process the chunks on both; compare the whole output stream per
+    channel (NaN positions exactly, the rest within REL_TOL of its maximum)."""
+    refs = [ref] if channels == 1 else ref
+    got, exp = [], []
+    for j, k in enumerate(chunks):
+        x = np.stack([white(rng, k) for _ in range(channels)])
+        for (jj, c, s) in nan_at:
+            if jj == j:
+                x[c, s] = np.nan
+        g = conv.process(x[0] if channels == 1 else x)
+        got.append(g.reshape(channels, k))
+        exp.append(np.stack([refs[c].process(x[c]) for c in range(channels)]))
+    got, exp = np.concatenate(got, axis=1), np.concatenate(exp, axis=1)
+    for c in range(channels):
+        assert np.array_equal(np.isnan(got[c]), np.isnan(exp[c])), f"channel {c}"
+        m = ~np.isnan(exp[c])
+        assert_close(got[c][m], exp[c][m], what=f"channel {c}")
+
+
+@pytest.mark.parametrize("head,L", [(64, 12000), (128, 20000), (256, 30000), (512, 40000)])
+def test_deferred_periods_vs_oracle(amd, oracle_mod, head, L):
+    """aligned calls only: every tail0 block deferred, several periods."""
+    rng = np.random.default_rng(head + L)
+    h = ir(rng, L)
+    conv = amd.TwoStageFFTConvolver.init(h, head, L)
+    ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
+    T = ref.tail_block_size
+    _run(conv, ref, rng, [head] * (3 * T // head + 7))
+
+
+def test_deferred_flush_on_unaligned_call(amd, oracle_mod):
+    rng = np.random.default_rng(6)
+    head, L = 64, 12000
+    h = ir(rng, L)
+    conv = amd.TwoStageFFTConvolver.init(h, head, L)
+    ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
+    T = ref.tail_block_size
+    per = T // head
+    chunks = [head] * (per + 5) + [13, 51] + [head] * (per - 3) + [7, 57, 64, 1, 63] + [head] * (2 * per)
+    _run(conv, ref, rng, chunks)
+
+
+def test_deferred_clone_and_reset_mid_period(amd, oracle_mod):
+    rng = np.random.default_rng(7)
+    head, L = 64, 12000
+    h = ir(rng, L)
+    conv = amd.TwoStageFFTConvolver.init(h, head, L)
+    ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
+    T = ref.tail_block_size
+    _run(conv, ref, rng, [head] * (T // head + 9))  # 9 blocks pending
+    twin = conv.clone()
+    for _ in range(2 * T // head):
+        x = white(rng, head)
+        a, b = conv.process(x), twin.process(x)
+        assert np.array_equal(a, b)
+        assert_close(a, ref.process(x), what="after clone")
+    _run(conv, ref, rng, [head] * 5)
+    conv.reset()
+    ref.reset()
+    _run(conv, ref, rng, [head] * (2 * T // head + 3))
+
+
+def test_deferred_nan_block_replays(amd, oracle_mod):
+    """a NaN sample in a pending block: tail0's C2R fails on that block, the
+    flush replays the period block by block (zero output for the failing
+    block, state frozen at it, as the reference)."""
+    rng = np.random.default_rng(8)
+    head, L = 64, 12000
+    h = ir(rng, L)
+    conv = amd.TwoStageFFTConvolver.init(h, head, L)
+    ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
+    T = ref.tail_block_size
+    per = T // head
+    _run(conv, ref, rng, [head] * (4 * per + 2), nan_at=[(per + 5, 0, 11), (2 * per + per - 1, 0, 3)])
+
+
+def test_deferred_batch_one_channel_replays(amd, oracle_mod):
+    """distinct channels; a non-finite block on one channel replays only that
+    channel's pending blocks."""
+    rng = np.random.default_rng(9)
+    head, L, C = 64, 10000, 4
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.TwoStageFFTConvolver.init(hs, head, L, channels=C)
+    ref = [oracle_mod.TwoStageFFTConvolver.init(hs[c], head, L) for c in range(C)]
+    T = ref[0].tail_block_size
+    per = T // head
+    _run(conv, ref, rng, [head] * (3 * per + 4), nan_at=[(per + 3, 2, 40)], channels=C)
