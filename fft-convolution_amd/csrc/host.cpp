@@ -620,6 +620,8 @@ struct TwoStageCore {
     DevPtr<float2> t0_xs;
     DevPtr<float> t0_ys;
     DevPtr<int> t0_err;
+    DevPtr<float> t0_ov;
+    DevPtr<float2> t0_cv;
     Scratch scratch;
     mutable StreamOrder order;
 
@@ -685,12 +687,15 @@ struct TwoStageCore {
         tail_output = out1.p; tail_precalculated = pre1.p;
         tin_idx = 0;
         static const bool defer = [] { const char *e = getenv("FFTCONV_TAIL0_DEFER"); return !e || atoi(e) != 0; }();
-        t0_defer = defer && tail0 && tail0->B == head_bs && tail0_defer_supported(tail0->log2b);
+        t0_nmax = T / std::max<size_t>(head_bs, 1);
+        t0_defer = defer && tail0 && tail0->B == head_bs &&
+                   tail0_defer_supported(tail0->log2b, (int)tail0->S, (int)t0_nmax);
         if (t0_defer) {
-            t0_nmax = T / head_bs;
             if (int r = t0_xs.alloc(C * t0_nmax * head_bs)) return r;
             if (int r = t0_ys.alloc(C * t0_nmax * 2 * head_bs)) return r;
             if (int r = t0_err.alloc(C)) return r;
+            if (int r = t0_ov.alloc(C * head_bs)) return r;
+            if (int r = t0_cv.alloc(C * t0_nmax * head_bs)) return r;
             HIP_TRY(hipMemsetAsync(t0_err.p, 0, t0_err.bytes(), stream));
         }
         t0_off = t0_n = 0;
@@ -704,7 +709,8 @@ struct TwoStageCore {
         a.pa.job[0] = tail0->job(tail_input() + t0_off, T, tail_output0 + t0_off, T, head_bs);
         a.pa.tw = tail0->tw.p;
         a.pa.njobs = 1;
-        a.xs = t0_xs.p; a.ys = t0_ys.p; a.err = t0_err.p;
+        a.xs = t0_xs.p; a.ys = t0_ys.p; a.err = t0_err.p; a.ov0 = t0_ov.p; a.cv = t0_cv.p;
+        a.act = (int)tail0->S;
         a.n = (int)t0_n; a.nmax = (int)t0_nmax;
         t0_n = 0;
         HIP_TRY(launch_tail0_flush(tail0->log2b, a, (int)C, s));

@@ -1368,71 +1368,197 @@ __global__ __launch_bounds__(64) void tail0_r2c_kernel(Tail0Args t) {
     float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);
     float2 *xr = t.xs + ((size_t)c * t.nmax + k) * B;
     for (int m = lane; m < B; m += 64) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
+    if (k == 0) {  // the overlap before the period's blocks, for (3) (whose tiles overwrite it)
+        for (int j = lane; j < B; j += 64) t.ov0[c * B + j] = J.overlap[c * B + j];
+    }
 }
 
 // (2) conv_k = sum_{i=1}^{act-1} H[i] (.) X_{k-i} + H[0] (.) X_k (:244-261,
-// the reference's row order) for a tile of KT blocks of one channel (thread
-// = block x slot; X_{k-i} is pending block k-i, or for i > k the FDL row
-// (cur0 + i - k) % act of the previous period, untouched so far), then the
-// C2R of each block (:264, one wave per block; the 1/N is applied by (3))
+// rows in the reference's order) for every pending block k, one slot chunk
+// of FC float4 per workgroup.  X_m is pending block m (m >= 0) or, for m < 0,
+// the FDL row (cur0 - m) % act of the previous period (untouched so far).
+// The chunk's IR rows and every X row it meets are staged in LDS once; a
+// thread owns one slot and J consecutive blocks and walks the rows with the
+// X values in a register ring (one H and one X read per row for J MACs).
+constexpr int T0_J = 8, T0_FC = 32;
+template <int LOG2B>
+__host__ __device__ constexpr size_t tail0_mac_lds(int act, int n) {
+    return (size_t)(2 * act - 1 + n) * T0_FC * 16;
+}
 template <int LOG2B>
 __global__ __launch_bounds__(256) void tail0_mac_kernel(Tail0Args t) {
-    constexpr int B = 1 << LOG2B, F = B / 2, KT = 256 / F;
+    constexpr int B = 1 << LOG2B, F = B / 2, FC = F < T0_FC ? F : T0_FC, J = T0_J, RS = J + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2 *twl = reinterpret_cast<float2 *>(smem), *zs = twl + 2 * B, *qs = zs + KT * B;
-    const ProcJob &J = t.pa.job[0];
+    const ProcJob &J0 = t.pa.job[0];
     const size_t c = blockIdx.x;
-    const int tid = threadIdx.x, kk = tid / F, f = tid % F;
-    const int k = blockIdx.y * KT + kk;
-    dma_16b<256>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
-    const int4 st = J.state[c];
-    const int cur0 = st.x, act = st.y;
-    const size_t rows = (size_t)J.S * B;
-    const float4 *H = reinterpret_cast<const float4 *>(J.H + c * rows);
-    const float4 *X = reinterpret_cast<const float4 *>(J.X + c * rows);
-    const float4 *xs = reinterpret_cast<const float4 *>(t.xs + (size_t)c * t.nmax * B);
-    if (k < t.n) {
-        Acc2 acc;
-        acc.zero();
-        for (int i = 1; i < act; ++i) {
-            const int m = k - i;
-            int r = cur0 + i - k;
-            if (r >= act) r -= act;
-            const float4 *xp = m >= 0 ? xs + (size_t)m * F : X + (size_t)r * F;
-            acc.mac(H[(size_t)i * F + f], xp[f]);
+    const int fc0 = blockIdx.y * FC;
+    const int tid = threadIdx.x, fl = tid % FC, g = tid / FC;
+    const int4 st = J0.state[c];
+    const int cur0 = st.x, act = st.y, n = t.n;
+    if (act != t.act) {  // (not a geometry the LDS was sized for: the replay path runs it)
+        if (tid == 0) t.err[c] = 1;
+        return;
+    }
+    const size_t rows = (size_t)J0.S * B;
+    const float4 *H = reinterpret_cast<const float4 *>(J0.H + c * rows) + fc0;
+    const float4 *X = reinterpret_cast<const float4 *>(J0.X + c * rows) + fc0;
+    const float4 *xs = reinterpret_cast<const float4 *>(t.xs + (size_t)c * t.nmax * B) + fc0;
+    float4 *Hs = reinterpret_cast<float4 *>(smem);  // [act][FC]
+    float4 *Xs = Hs + (size_t)act * FC;              // [act - 1 + n][FC]: q = m + act - 1
+    const int nq = act - 1 + n;
+    // LDS-DMA of every row chunk (no VGPRs, all in flight): a wave copies
+    // two rows per instruction, lanes 0..31 the first, 32..63 the second
+    static_assert(FC == 32, "a row chunk is half a wave of 16-byte lanes");
+    {
+        const int wave = tid >> 6, lane = tid & 63, half = lane >> 5, f = lane & 31;
+        const int nrows = act + nq;
+        for (int r2 = wave * 2; r2 < nrows; r2 += 8) {
+            const int row = min(r2 + half, nrows - 1);  // (an odd last row: both halves copy it)
+            const float4 *src;
+            if (row < act) {
+                src = H + (size_t)row * F;
+            } else {
+                const int q = row - act;
+                if (q < act - 1) {
+                    int r = cur0 + act - 1 - q;
+                    if (r >= act) r -= act;
+                    src = X + (size_t)r * F;
+                } else {
+                    src = xs + (size_t)(q - (act - 1)) * F;
+                }
+            }
+            if (r2 + half < nrows || half == 0)
+                __builtin_amdgcn_global_load_lds((gptr_t)(src + f), (lptr_t)(Hs + (size_t)r2 * FC), 16, 0, 0);
         }
-        const float4 cv = slot_mac(acc.get(f), xs[(size_t)k * F + f], H[f], f);
-        reinterpret_cast<float4 *>(zs + kk * B)[f] = cv;
-        if (f == 0 && !slot0_finite(cv)) t.err[c] = 1;  // realfft's C2R error (:264-267)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int wave = tid >> 6, lane = tid & 63;
-    float2 *q = qs + wave * B;
-    for (int b = wave; b < KT; b += 4) {
-        const int kb = blockIdx.y * KT + b;
-        if (kb >= t.n) break;
-        float2 *Z = zs + b * B;
-        for (int m = lane; m < B; m += 64) q[m] = real_pre<LOG2B, 64>(Z, m, twl);
-        wave_sync();
-        const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(q, Z, twl));
-        float *yr = t.ys + ((size_t)c * t.nmax + kb) * 2 * B;
-        for (int j = lane; j < 2 * B; j += 64) yr[j] = y[j];
-        wave_sync();
+    const int kb0 = g * J;
+    if (kb0 >= n) return;
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto xq = [&](int q) { return (q >= 0 && q < nq) ? Xs[(size_t)q * FC + fl] : zero4; };
+    LaAcc acc[J];  // (packed FMAs, la.hpp)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j].zero();
+    const bool z0 = fc0 + fl == 0;
+    // load e of the walk is X at q = Q1 + J - 1 - e; row i = s + 1 of step s
+    // meets, for block kb0 + j, load e = s + J - 1 - j
+    const int Q1 = kb0 + act - 2;
+    float4 xr[RS];
+#pragma unroll
+    for (int e = 0; e < J; ++e) xr[e] = xq(Q1 + J - 1 - e);
+    float4 hn = act > 1 ? Hs[FC + fl] : zero4;
+    const int ns = act - 1;
+    for (int s0 = 0; s0 < ns; s0 += RS) {
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+            const int sidx = s0 + u;
+            if (sidx >= ns) break;
+            const float4 h = hn;
+            xr[(u + J) % RS] = xq(Q1 - 1 - sidx);
+            hn = sidx + 2 < act ? Hs[(size_t)(sidx + 2) * FC + fl] : zero4;
+            const LaH ho = la_ops(h, z0);
+#pragma unroll
+            for (int j = 0; j < J; ++j) acc[j].mac(ho, xr[(u + J - 1 - j) % RS]);
+        }
+    }
+    const float4 h0 = Hs[fl];
+    const int f = fc0 + fl;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int k = kb0 + j;
+        if (k < n) {
+            const float4 cv = slot_mac(acc[j].get(), Xs[(size_t)(k + act - 1) * FC + fl], h0, f);
+            reinterpret_cast<float4 *>(t.cv + ((size_t)c * t.nmax + k) * B)[f] = cv;
+        }
     }
 }
 
-// (3) per channel: overlap-add (:270-274) and overlap save (:283-284) over
-// the pending blocks, the FDL rows (block k at (cur0 - k) % act; the last
-// act blocks stay), current and the flags -- or, if any block's C2R failed,
-// tail_convolver0.process block by block (:464-472) from the untouched state
-// by the generic step, so errors leave exactly the reference's state
+// (2b) the C2R of conv_k (:264, the 1/N applied by (3)), one wave per block;
+// realfft's C2R error (a non-finite DC / Nyquist bin, :264-267) flags the
+// channel for (4)
 template <int LOG2B>
-__device__ __attribute__((noinline)) void tail0_replay(const Tail0Args *tp, size_t c, unsigned char *smem) {
-    constexpr int B = 1 << LOG2B, NT = proc_nt(LOG2B);
-    const Tail0Args &t = *tp;
+__global__ __launch_bounds__(64) void tail0_c2r_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2 *Z = reinterpret_cast<float2 *>(smem), *q = Z + B, *twl = q + B;
+    const size_t c = blockIdx.x;
+    const int k = blockIdx.y, lane = threadIdx.x;
+    const float2 *cr = t.cv + ((size_t)c * t.nmax + k) * B;
+    dma_16b<64>(Z, cr, B * (int)sizeof(float2));
+    dma_16b<64>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    if (lane == 0 && !(isfinite(Z[0].x) && isfinite(Z[0].y))) t.err[c] = 1;
+    for (int m = lane; m < B; m += 64) q[m] = real_pre<LOG2B, 64>(Z, m, twl);
+    wave_sync();
+    const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(q, Z, twl));
+    float *yr = t.ys + ((size_t)c * t.nmax + k) * 2 * B;
+    for (int j = lane; j < 2 * B; j += 64) yr[j] = y[j];
+}
+
+// (3) overlap-add (:270-274) over a tile of pending blocks, the overlap
+// save (:283-284) by the last tile, and the FDL rows (:229-241; block k at
+// (cur0 - k) % act, the last act blocks stay) -- channels without a C2R error
+template <int LOG2B>
+__global__ __launch_bounds__(256) void tail0_commit_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B, KT = 256 / (B / 2), NT = 256;
+    constexpr float invN = 1.0f / (float)(2 * B);
     const ProcJob &J = t.pa.job[0];
-    for (int k = 0; k < t.n; ++k) {
+    const size_t c = blockIdx.x;
+    if (t.err[c]) return;  // (replayed by tail0_replay_kernel)
+    const int tid = threadIdx.x, n = t.n;
+    const int k0 = blockIdx.y * KT, k1 = min(n, k0 + KT);
+    const int4 st = J.state[c];
+    const int cur0 = st.x, act = st.y;
+    const float *ys = t.ys + (size_t)c * t.nmax * 2 * B;
+    float *outc = J.out + c * J.out_stride;
+    for (int idx = k0 * B + tid; idx < k1 * B; idx += NT) {
+        const int k = idx >> LOG2B, j = idx & (B - 1);
+        const float ov = k == 0 ? t.ov0[c * B + j] : ys[(size_t)(k - 1) * 2 * B + B + j] * invN;
+        outc[idx] = ys[(size_t)k * 2 * B + j] * invN + ov;
+    }
+    if (k1 == n) {  // (the input buffer is empty after a completed block, :280)
+        for (int j = tid; j < B; j += NT) J.overlap[c * B + j] = ys[(size_t)(n - 1) * 2 * B + B + j] * invN;
+        if (st.w & FLAG_INBUF)
+            for (int j = tid; j < B; j += NT) J.inbuf[c * B + j] = 0.f;
+    }
+    const size_t rows = (size_t)J.S * B;
+    float2 *Xc = J.X + c * rows;
+    const float2 *xs = t.xs + (size_t)c * t.nmax * B;
+    const int kf = max(k0, n - act);
+    for (int idx = tid; idx < (k1 - kf) * B; idx += NT) {
+        const int k = kf + (idx >> LOG2B), m = idx & (B - 1);
+        int r = (cur0 - k) % act;
+        if (r < 0) r += act;
+        Xc[(size_t)r * B + m] = xs[(size_t)k * B + m];
+    }
+}
+
+// (4) per channel: the state word of a committed channel (current, the
+// flags of n completed blocks) -- or, for a channel whose C2R failed on a
+// pending block, tail_convolver0.process block by block (:464-472) from the
+// untouched state by the generic step, so the failing block leaves exactly
+// the reference's state
+template <int LOG2B>
+__global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_replay_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B, NT = proc_nt(LOG2B);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ProcJob &J = t.pa.job[0];
+    const size_t c = blockIdx.x;
+    const int n = t.n;
+    if (!t.err[c]) {
+        if (threadIdx.x == 0) {
+            const int4 st = J.state[c];
+            const int act = st.y;
+            int cur = (st.x - n) % act;
+            if (cur < 0) cur += act;
+            const int flags = (st.w & ~(FLAG_PRE | FLAG_INBUF)) ^ ((n & 1) ? FLAG_REV : 0);
+            J.state[c] = make_int4(cur, act, 0, la_clear(flags, t.pa));
+        }
+        return;
+    }
+    for (int k = 0; k < n; ++k) {
         ProcJob Jk = J;
         Jk.in = J.in + (size_t)k * B;
         Jk.out = J.out + (size_t)k * B;
@@ -1443,51 +1569,6 @@ __device__ __attribute__((noinline)) void tail0_replay(const Tail0Args *tp, size
     }
     __syncthreads();
     if (threadIdx.x == 0) t.err[c] = 0;
-}
-template <int LOG2B>
-__global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_finish_kernel(Tail0Args t) {
-    constexpr int B = 1 << LOG2B, NT = proc_nt(LOG2B);
-    constexpr float invN = 1.0f / (float)(2 * B);
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const ProcJob &J = t.pa.job[0];
-    const size_t c = blockIdx.x;
-    const int tid = threadIdx.x, n = t.n;
-    if (t.err[c]) {  // (the arguments by their kernarg address: no private copy)
-        tail0_replay<LOG2B>((const Tail0Args *)__builtin_amdgcn_kernarg_segment_ptr(), c, smem);
-        return;
-    }
-    const int4 st = J.state[c];
-    const int cur0 = st.x, act = st.y;
-    const float *ys = t.ys + (size_t)c * t.nmax * 2 * B;
-    float *outc = J.out + c * J.out_stride;
-    float *ovc = J.overlap + c * B;
-    for (int idx = tid; idx < n * B; idx += NT) {
-        const int k = idx >> LOG2B, j = idx & (B - 1);
-        const float ov = k == 0 ? ovc[j] : ys[(size_t)(k - 1) * 2 * B + B + j] * invN;
-        outc[idx] = ys[(size_t)k * 2 * B + j] * invN + ov;
-    }
-    __syncthreads();  // every read of the old overlap is done
-    for (int j = tid; j < B; j += NT) ovc[j] = ys[(size_t)(n - 1) * 2 * B + B + j] * invN;
-    if (st.w & FLAG_INBUF) {  // a completed block empties the input buffer (:280)
-        float *ibc = J.inbuf + c * B;
-        for (int j = tid; j < B; j += NT) ibc[j] = 0.f;
-    }
-    const size_t rows = (size_t)J.S * B;
-    float2 *Xc = J.X + c * rows;
-    const float2 *xs = t.xs + (size_t)c * t.nmax * B;
-    const int k0 = n > act ? n - act : 0;
-    for (int idx = tid; idx < (n - k0) * B; idx += NT) {
-        const int k = k0 + (idx >> LOG2B), m = idx & (B - 1);
-        int r = (cur0 - k) % act;
-        if (r < 0) r += act;
-        Xc[(size_t)r * B + m] = xs[(size_t)k * B + m];
-    }
-    if (tid == 0) {
-        int cur = (cur0 - n) % act;
-        if (cur < 0) cur += act;
-        const int flags = (st.w & ~(FLAG_PRE | FLAG_INBUF)) ^ ((n & 1) ? FLAG_REV : 0);
-        J.state[c] = make_int4(cur, act, 0, la_clear(flags, t.pa));
-    }
 }
 
 static int g_variant = VARIANT_AUTO;
@@ -1562,16 +1643,31 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
         t.pa.pipe = (var & VARIANT_NOPIPE) ? 0 : 1;  // (the replay path's generic step)
         t.pa.lag = pipeline_lag(LOG2B);
         hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
-        hipLaunchKernelGGL(tail0_mac_kernel<LOG2B>, dim3(channels, (a.n + KT - 1) / KT), dim3(256),
-                           (size_t)(6 + KT) * B * sizeof(float2), s, t);
-        constexpr size_t fin_lds = Geo<LOG2B, NT>::lds_bytes;  // (the replay path's generic step)
-        hipLaunchKernelGGL(tail0_finish_kernel<LOG2B>, dim3(channels), dim3(NT), fin_lds, s, t);
+        {
+            constexpr int F = B / 2, FC = F < T0_FC ? F : T0_FC;
+            const size_t lds = tail0_mac_lds<LOG2B>(a.act, a.n);
+            auto mk = tail0_mac_kernel<LOG2B>;
+            if (lds > 160 * 1024 || (256 / FC) * T0_J < a.n) return hipErrorInvalidValue;
+            if (lds > 64 * 1024) {
+                hipError_t e = hipFuncSetAttribute((const void *)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(mk, dim3(channels, F / FC), dim3(256), lds, s, t);
+        }
+        hipLaunchKernelGGL(tail0_c2r_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
+        hipLaunchKernelGGL(tail0_commit_kernel<LOG2B>, dim3(channels, (a.n + KT - 1) / KT), dim3(256), 0, s, t);
+        constexpr size_t rep_lds = Geo<LOG2B, NT>::lds_bytes;  // (the generic step)
+        hipLaunchKernelGGL(tail0_replay_kernel<LOG2B>, dim3(channels), dim3(NT), rep_lds, s, t);
         return hipGetLastError();
     } else {
         return hipErrorNotSupported;
     }
 }
-bool tail0_defer_supported(int log2b) { return log2b >= 6 && log2b <= 9; }
+bool tail0_defer_supported(int log2b, int act, int nmax) {
+    if (log2b < 6 || log2b > 9 || act < 1 || nmax < 1) return false;
+    const int F = (1 << log2b) / 2, FC = F < T0_FC ? F : T0_FC;
+    return nmax <= (256 / FC) * T0_J && tail0_mac_lds<6>(act, nmax) <= 160 * 1024;
+}
 hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;
     switch (log2b) {

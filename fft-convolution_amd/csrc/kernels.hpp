@@ -210,10 +210,13 @@ struct Tail0Args {
     float2 *xs;            // [C][nmax][B]: spectra of the pending blocks
     float *ys;             // [C][nmax][2B]: their C2R outputs (not yet scaled)
     int *err;              // [C]: some pending block's C2R fails
+    float *ov0;            // [C][B]: the overlap before the pending blocks
+    float2 *cv;            // [C][nmax][B]: conv of each pending block
+    int act;               // tail0's active segments (every channel: TwoStage never updates tail0)
     int n;                 // pending blocks
     int nmax;              // row pitch of xs / ys in blocks
 };
-bool tail0_defer_supported(int log2b);
+bool tail0_defer_supported(int log2b, int act, int nmax);
 hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s);
 
 constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)
