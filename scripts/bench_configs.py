@@ -46,6 +46,16 @@ def uniform_bytes(B, L):
     return 16 * S * K + 8 * K + 16 * B  # per channel-block
 
 
+def tail0_deferred_bytes_per_block(head, T):
+    """tail0 deferred to the period end (csrc/kernels.hip tail0_*_kernel), per
+    channel and head block, in rows of 8*head bytes: over a period of n = T/head
+    blocks the flush reads the S0 = T/head IR rows and S0-1 FDL rows once, and
+    per block writes / reads its spectrum (R2C, MAC, commit: 4 rows incl. the
+    FDL write), its conv (2), its C2R output (2), input and output (1)."""
+    n = S0 = T // head
+    return (2 * S0 - 1 + 9 * n) * 8 * head / n
+
+
 def run(conv, C, n_in, n_out, steps, warmup, ring, stream, update=None, batched=False):
     """One process() call per step.  batched: the calls of a ring pass are issued
     by one process_device_steps host call (same kernels, no per-call Python
@@ -178,7 +188,10 @@ def main():
         conv = F.TwoStageFFTConvolver.init(shard.synth_irs(range(C), L), head, L, channels=C)
         T = conv.tail_block_size
         samples = C * head * a.steps3
-        per_sample = (uniform_bytes(head, T) + uniform_bytes(head, T) + uniform_bytes(T, L - 2 * T) * head / T) / head
+        canon_sample = (uniform_bytes(head, T) + uniform_bytes(head, T) + uniform_bytes(T, L - 2 * T) * head / T) / head
+        defer = os.environ.get("FFTCONV_TAIL0_DEFER", "1") != "0"  # (host.cpp TwoStageCore::t0_defer)
+        tail0_b = tail0_deferred_bytes_per_block(head, T) if defer else uniform_bytes(head, T)
+        per_sample = (uniform_bytes(head, T) + tail0_b + uniform_bytes(T, L - 2 * T) * head / T) / head
         if a.sweep:
             sets = [dict(kv.split("=") for kv in part.split(",") if kv) for part in a.sweep.split(";")]
             times = [[] for _ in sets]
@@ -202,7 +215,11 @@ def main():
                         "us_per_step": round(t / a.steps3 * 1e6, 3),
                         "algorithmic_GBs": round(samples * per_sample / t / 1e9, 1),
                         "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
-                        "bytes_per_sample": round(per_sample, 1)})
+                        "bytes_per_sample": round(per_sample, 1),
+                        "canonical_bytes_per_sample": round(canon_sample, 1),
+                        "path": "head: one fused launch per call; tail0 deferred to the period end (one pass per "
+                                "period); tail: side stream" if tail0_b != uniform_bytes(head, T) else
+                                "head + tail0: one launch per call; tail: side stream"})
         del conv
         if not a.no_cpu and not a.pmc_inner:
             out[-1]["cpu_baseline"] = cpu_baseline("twostage", C, head, L)

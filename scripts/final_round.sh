@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-end measurement set (run on the GPU box): GPU tests, headline bench,
+# rocprofv3 kernel stats + PMC passes of the bench, cfg3/cfg5 with cpu
+# baselines and per-kernel PMC.  Usage: scripts/final_round.sh TAG
+set -u
+tag=$1
+scripts/gpu_step.sh ${tag}_gputest 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread || exit $?
+grep -q " passed" gpurun_out/${tag}_gputest.log && ! grep -q "failed" gpurun_out/${tag}_gputest.log || exit 5
+scripts/gpu_step.sh ${tag}_bench 300 python bench.py || exit $?
+scripts/profile.sh $tag || exit $?
+scripts/gpu_step.sh ${tag}_configs 600 python scripts/bench_configs.py --configs 3,5 --pmc || exit $?
