@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(64) void tail0_r2c_kernel(Tail0Args t) {
 constexpr int T0_J = 8, T0_FC = 32;
 template <int LOG2B>
 __host__ __device__ constexpr size_t tail0_mac_lds(int act, int n) {
-    return (size_t)(2 * act - 1 + n) * T0_FC * 16;
+    return (size_t)(2 * act + 1 + n + T0_J) * T0_FC * 16;  // (+ zero rows: H[act], X[-1], X[nq..nq+J))
 }
 template <int LOG2B>
 __global__ __launch_bounds__(256) void tail0_mac_kernel(Tail0Args t) {
@@ -1403,40 +1403,45 @@ __global__ __launch_bounds__(256) void tail0_mac_kernel(Tail0Args t) {
     const float4 *H = reinterpret_cast<const float4 *>(J0.H + c * rows) + fc0;
     const float4 *X = reinterpret_cast<const float4 *>(J0.X + c * rows) + fc0;
     const float4 *xs = reinterpret_cast<const float4 *>(t.xs + (size_t)c * t.nmax * B) + fc0;
-    float4 *Hs = reinterpret_cast<float4 *>(smem);  // [act][FC]
-    float4 *Xs = Hs + (size_t)act * FC;              // [act - 1 + n][FC]: q = m + act - 1
+    // LDS: H rows [0, act) and a zero row; then X rows q = m + act - 1 in
+    // [-1, nq + J) (q = -1 and q >= nq zero), so the walk reads unguarded
     const int nq = act - 1 + n;
+    float4 *Hs = reinterpret_cast<float4 *>(smem);  // [act + 1][FC]
+    float4 *Xs = Hs + (size_t)(act + 2) * FC;        // Xs[q * FC], q >= -1
+    for (int idx = tid; idx < FC; idx += 256) Hs[(size_t)act * FC + idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int idx = tid; idx < (J + 1) * FC; idx += 256) {
+        const int q = idx < FC ? -1 : nq + idx / FC - 1;
+        Xs[(size_t)q * FC + idx % FC] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     // LDS-DMA of every row chunk (no VGPRs, all in flight): a wave copies
     // two rows per instruction, lanes 0..31 the first, 32..63 the second
     static_assert(FC == 32, "a row chunk is half a wave of 16-byte lanes");
     {
         const int wave = tid >> 6, lane = tid & 63, half = lane >> 5, f = lane & 31;
-        const int nrows = act + nq;
-        for (int r2 = wave * 2; r2 < nrows; r2 += 8) {
-            const int row = min(r2 + half, nrows - 1);  // (an odd last row: both halves copy it)
+        for (int r2 = wave * 2; r2 < act; r2 += 8) {  // IR rows
+            if (r2 + half < act)
+                __builtin_amdgcn_global_load_lds((gptr_t)(H + (size_t)(r2 + half) * F + f),
+                                                 (lptr_t)(Hs + (size_t)r2 * FC), 16, 0, 0);
+        }
+        for (int r2 = wave * 2; r2 < nq; r2 += 8) {  // X rows
+            const int q = r2 + half;
             const float4 *src;
-            if (row < act) {
-                src = H + (size_t)row * F;
+            if (q < act - 1) {
+                int r = cur0 + act - 1 - q;
+                if (r >= act) r -= act;
+                src = X + (size_t)r * F;
             } else {
-                const int q = row - act;
-                if (q < act - 1) {
-                    int r = cur0 + act - 1 - q;
-                    if (r >= act) r -= act;
-                    src = X + (size_t)r * F;
-                } else {
-                    src = xs + (size_t)(q - (act - 1)) * F;
-                }
+                src = xs + (size_t)(q - (act - 1)) * F;
             }
-            if (r2 + half < nrows || half == 0)
-                __builtin_amdgcn_global_load_lds((gptr_t)(src + f), (lptr_t)(Hs + (size_t)r2 * FC), 16, 0, 0);
+            if (q < nq)
+                __builtin_amdgcn_global_load_lds((gptr_t)(src + f), (lptr_t)(Xs + (size_t)r2 * FC), 16, 0, 0);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int kb0 = g * J;
     if (kb0 >= n) return;
-    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto xq = [&](int q) { return (q >= 0 && q < nq) ? Xs[(size_t)q * FC + fl] : zero4; };
+    auto xq = [&](int q) { return Xs[q * FC + fl]; };  // (q in [-1, nq + J): zero rows at the ends)
     LaAcc acc[J];  // (packed FMAs, la.hpp)
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j].zero();
@@ -1447,7 +1452,7 @@ __global__ __launch_bounds__(256) void tail0_mac_kernel(Tail0Args t) {
     float4 xr[RS];
 #pragma unroll
     for (int e = 0; e < J; ++e) xr[e] = xq(Q1 + J - 1 - e);
-    float4 hn = act > 1 ? Hs[FC + fl] : zero4;
+    float4 hn = Hs[(size_t)min(1, act) * FC + fl];
     const int ns = act - 1;
     for (int s0 = 0; s0 < ns; s0 += RS) {
 #pragma unroll
@@ -1456,7 +1461,7 @@ __global__ __launch_bounds__(256) void tail0_mac_kernel(Tail0Args t) {
             if (sidx >= ns) break;
             const float4 h = hn;
             xr[(u + J) % RS] = xq(Q1 - 1 - sidx);
-            hn = sidx + 2 < act ? Hs[(size_t)(sidx + 2) * FC + fl] : zero4;
+            hn = Hs[(size_t)min(sidx + 2, act) * FC + fl];  // (row act is zero)
             const LaH ho = la_ops(h, z0);
 #pragma unroll
             for (int j = 0; j < J; ++j) acc[j].mac(ho, xr[(u + J - 1 - j) % RS]);
