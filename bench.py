@@ -6,10 +6,10 @@ channels per GPU, block 256, a distinct 48,000-tap white-noise IR per channel,
 f32.  One *step* = one FFTConvolver::process call of 256 samples on every
 channel (src/fft_convolver.rs:215-295) = one fused kernel launch: forward R2C
 of the new block into the FDL, the S-segment spectral MAC, C2R and overlap-add
--- with the lookahead step (csrc/la.hpp) each step sums only the 5 nearest
-FDL rows itself; rows 6..32 are summed 5 blocks ahead by mid anchors (C/5
-channels per launch) and rows >= 33 thirty-two blocks ahead by far anchors
-(C/32 channels per launch), S >= 40.  The timed steps are submitted through
+-- with the lookahead step (csrc/la.hpp) each step sums only the 4 nearest
+FDL rows itself; rows 5..16 are summed 4 blocks ahead (C/4 channels per
+launch), rows 17..64 sixteen blocks ahead (C/16) and rows >= 65 sixty-four
+blocks ahead (C/64) by anchors, S >= 40.  The timed steps are submitted through
 process_device_steps (the C ABI loops over the calls), not one Python call each.
 Inputs are resident in HBM when the timed region starts.
 
@@ -50,31 +50,40 @@ def algorithmic_bytes_per_channel_block(B: int, L: int) -> int:
     return 16 * S * K + 8 * K + 4 * B + 4 * B + 8 * B
 
 
-LA_D1, LA_DM, LA_DF = 5, 5, 32  # lookahead levels (fft-convolution_amd/csrc/la.hpp)
-LA_NEAR_NEXT_MIN_B = 512  # la.hpp near_next(): B > 256 (no in-step mid anchors) stores the next near sum
+# lookahead levels (fft-convolution_amd/csrc/la.hpp): near rows 1..D0; anchor
+# level k sums rows (R_{k-1}, R_k] every P_k blocks (R_0 = D0, R_3 = S - 1)
+LA_D0 = 4
+LA_LEVELS = ((4, 16), (16, 64), (64, None))  # (P_k, R_k)
+LA_NEAR_NEXT_MIN_B = 512  # la.hpp near_next(): B > 256 (no in-step level-1 anchors) stores the next near sum
 
 
-def lookahead_bytes_per_channel_block(B: int, L: int, parts: int) -> int:
+def lookahead_bytes_per_channel_block(B: int, L: int) -> int:
     """Bytes per channel-block the lookahead step (la.hpp) reads and writes, in
     the units of SURVEY.md §8(d) (rows of K = B+1 bins, 8 B per bin):
-      far anchor every DF blocks: far H rows [DF+1, S) and FDL ages [1, S-2]
-        once: 8K (2S - DF - 3) / DF;
-      mid anchor every DM blocks: H rows [D1+1, DF] and ages [1, DF-1]:
-        8K (2 DF - D1 - 1) / DM;
-      near rows (step): H[1..D1] and the last D1 blocks: 8K * 2 D1;
-      window rows written by the anchors and read by the steps: 16K (parts + 1);
+      anchor level k (period P, rows lo..hi, an anchor every P blocks): H rows
+        lo..hi and FDL ages 1..hi-1 once: 8K (2 hi - lo) / P -- level 3 only
+        when S > 65 (la_nlv);
+      near rows (step): H[1..D0] and the last D0 blocks: 8K * 2 D0;
+      window rows written by the anchors and read by the steps: 16K per level;
       the new X row, H[0], in, out, overlap r/w: 16K + 16B.
     At B >= 512 the helpers also store the next block's near sum (la.hpp
     near_next): per block one more row read and one written, one FDL row
     fewer read (this block's spectrum comes from LDS): + 8K.
-    cfg2 (parts 1): 82,750 B, against 779,208 B for the reference's
-    algorithm (every block streams all S rows of H and of the FDL)."""
+    cfg2: 75,060 B (round 2's three levels: 82,750 B), against 779,208 B for
+    the reference's algorithm (every block streams all S rows of H and of the
+    FDL)."""
     S = -(-L // B)
     K = B + 1
-    far = 8 * K * (2 * S - LA_DF - 3) // LA_DF
-    mid = 8 * K * (2 * LA_DF - LA_D1 - 1) // LA_DM
-    near = 8 * K * 2 * LA_D1 + (8 * K if B >= LA_NEAR_NEXT_MIN_B else 0)
-    return far + mid + near + 16 * K * (parts + 1) + 16 * K + 16 * B
+    total = 0.0
+    lo = LA_D0 + 1
+    for P, R in LA_LEVELS:
+        hi = S - 1 if R is None else min(R, S - 1)
+        if hi < lo:
+            break
+        total += 8 * K * (2 * hi - lo) / P + 16 * K
+        lo = hi + 1
+    near = 8 * K * 2 * LA_D0 + (8 * K if B >= LA_NEAR_NEXT_MIN_B else 0)
+    return int(total + near + 16 * K + 16 * B)
 
 
 def parse():
@@ -337,9 +346,10 @@ def main():
     canonical_bytes = algorithmic_bytes_per_channel_block(B, L) * C
     parts = conv.lookahead_parts()
     if parts:
-        bytes_per_launch = lookahead_bytes_per_channel_block(B, L, parts) * C
-        kname = (f"upols_la_kernel (lookahead step: step workgroups of 2 channels + far anchors for "
-                 f"{C}/{LA_DF} and mid anchors for {C}/{LA_DM} channels per launch)")
+        bytes_per_launch = lookahead_bytes_per_channel_block(B, L) * C
+        kname = (f"upols_la_kernel (lookahead step: step workgroups of 2 channels running the level-1 "
+                 f"anchors of {C}/4 channels + level-2 anchors for {C}/16 and level-3 anchors for {C}/64 "
+                 f"channels per launch)")
     else:
         bytes_per_launch = canonical_bytes
         kname = "upols_process_kernel (fused UPOLS step, one workgroup per channel)"

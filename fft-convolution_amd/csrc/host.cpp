@@ -226,7 +226,7 @@ struct UniformCore {
     // lookahead (la.hpp): standalone batches only (la_ok, set before init)
     bool la_ok = false;
     int la_W = 0;                 // far parts (partial rows per step), 0 = off
-    DevPtr<float2> laP, laPm;     // far [C][2][DF][la_W][B] / mid [C][2][DM][B] windows
+    DevPtr<float2> laW;           // windows of the three anchor levels [C][2][LA_PT][B]
     unsigned long long la_t = 0;  // lookahead launches so far (stagger clock)
     // launch timelines of the last `trace_slots` lookahead launches (tuning
     // only: FFTCONV_LA_TRACE=<slots>, written to FFTCONV_LA_TRACE_OUT at destroy)
@@ -286,12 +286,11 @@ struct UniformCore {
         if (int r = hstage.alloc(C * ir_len)) return r;
         la_W = la_ok ? la_parts(log2b, (int)S) : 0;
         if (la_W) {
-            const LaDims d = la_dims(log2b);
-            if (int r = laP.alloc(C * 2 * (size_t)d.DF * (size_t)la_W * B)) return r;
-            if (int r = laPm.alloc(C * 2 * (size_t)d.DM * B)) return r;
+            const LaDims d = la_dims(log2b, (int)S);
+            if (int r = laW.alloc(C * 2 * (size_t)d.pt * B)) return r;
             if (const char *e = getenv("FFTCONV_LA_TRACE")) {
                 trace_slots = (size_t)std::max(0, atoi(e));
-                trace_grid = (C + 7) / 8 * 8 * (size_t)d.wg_far + C + C + 8;
+                trace_grid = (size_t)la_trace_grid(log2b, (int)S, (int)C);
                 if (trace_slots) {
                     if (int r = trace.alloc(trace_slots * trace_grid * 8)) return r;
                     HIP_TRY(hipMemset(trace.p, 0, trace.bytes()));
@@ -342,15 +341,12 @@ struct UniformCore {
     // one; without the lookahead step (or with VARIANT_LAFULL) nothing to do
     int la_rebuild(hipStream_t s, size_t chan0, size_t nch) {
         if (!la_W || la_parts(log2b, (int)S) != la_W || la_full_variant() || nch == 0) return FFTCONV_OK;
-        const LaDims d = la_dims(log2b);
-        const unsigned long long per = (unsigned long long)(d.DF * d.DM);
+        const unsigned long long per = (unsigned long long)la_dims(log2b, (int)S).per_all;
         ProcArgs a{};
         a.job[0] = job(nullptr, 0, nullptr, 0, B);
         a.tw = tw.p;
         a.njobs = 1;
-        a.laP = laP.p;
-        a.laPm = laPm.p;
-        a.la_W = la_W;
+        a.laW = laW.p;
         a.la_c0 = (int)chan0;
         a.la_t = (int)((la_t + per - 1) % per);
         HIP_TRY(launch_la_rebuild(log2b, a, (int)(chan0 + nch), s));
@@ -450,23 +446,14 @@ struct UniformCore {
     // a full-block call takes the lookahead launch
     bool la_ready(size_t n) const { return la_W && n == B && la_parts(log2b, (int)S) == la_W; }
 
-    // this batch's lookahead fields of a launch: windows, stagger clock,
-    // anchor workgroup counts (and the timeline record, when tracing)
+    // this batch's lookahead fields of a launch: windows, stagger clock (the
+    // launcher derives the anchor workgroups from them), and the timeline
+    // record, when tracing
     int la_fill(ProcArgs &a, hipStream_t s) {
-        const LaDims d = la_dims(log2b);
-        auto count = [&](size_t P) {
-            const size_t t0 = (size_t)(la_t % P);
-            return la_all ? C : (C > t0 ? (C - t0 + P - 1) / P : 0);
-        };
-        a.laP = laP.p;
-        a.laPm = laPm.p;
-        a.la_W = la_W;
+        a.laW = laW.p;
         a.la_all = la_all ? 1 : 0;
-        a.la_t = (int)(la_t % (unsigned long long)(d.DF * d.DM));  // (both periods divide it)
+        a.la_t = (int)(la_t % (unsigned long long)la_dims(log2b, (int)S).per_all);  // (every period divides it)
         a.la_seq = la_seq;
-        // (far anchors: whole rounds of 8 channels, one XCD each -- see la_anchor_far)
-        a.la_nfar = (int)((count((size_t)d.DF) + 7) / 8 * 8 * (size_t)d.wg_far);
-        a.la_nmid = d.mid_in_step ? 0 : (int)count((size_t)d.DM);
         if (trace_slots) {
             const size_t slot = (size_t)(la_t % trace_slots);
             a.la_trace = trace.p + slot * trace_grid * 8;
@@ -545,8 +532,7 @@ struct UniformCore {
         if (int r = cp(overlap, o.overlap)) return r;
         if (int r = cp(inbuf, o.inbuf)) return r;
         if (int r = cp(state, o.state)) return r;
-        if (int r = cp(laP, o.laP)) return r;
-        if (int r = cp(laPm, o.laPm)) return r;
+        if (int r = cp(laW, o.laW)) return r;
         la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
         if (o.trace_slots) {  // (tuning: a clone keeps its own timeline)
             trace_slots = o.trace_slots;
@@ -644,8 +630,9 @@ struct TwoStageCore {
         return FFTCONV_OK;
     }
 
-    // The side stream is confined to the first ncu/k CUs (k =
-    // FFTCONV_TAIL_CU_DIV, default 3): a T-block tail workgroup fills a whole
+    // The side stream is confined to the first ncu/k CUs (k = the tail's
+    // share of the bytes, 3 at cfg3; the r1 sweep over k = 1..6 is in
+    // profiles/r1/cfg3_tail_cu_div*.log): a T-block tail workgroup fills a whole
     // CU (1024 lanes x 128 VGPRs), and unconfined it locks the
     // latency-critical head steps out of the chip for its whole duration
     // (measured: a 197 us head step behind a 193 us tail).  Contiguous masks
@@ -662,7 +649,6 @@ struct TwoStageCore {
             k = (int)std::lround(per_b / std::max(tail_b, 1.0));
             k = std::min(8, std::max(2, k));
         }
-        if (const char *e = getenv("FFTCONV_TAIL_CU_DIV")) k = std::max(1, atoi(e));
         int ncu = 0;
         HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         if (k <= 1 || ncu <= 0) {
@@ -686,7 +672,7 @@ struct TwoStageCore {
         tail_output0 = out0.p; tail_precalculated0 = pre0.p;
         tail_output = out1.p; tail_precalculated = pre1.p;
         tin_idx = 0;
-        static const bool defer = [] { const char *e = getenv("FFTCONV_TAIL0_DEFER"); return !e || atoi(e) != 0; }();
+        const bool defer = tail0_defer_allowed();  // (VARIANT_T0BLOCK: per-block tail0, tests)
         t0_nmax = T / std::max<size_t>(head_bs, 1);
         t0_defer = defer && tail0 && tail0->B == head_bs &&
                    tail0_defer_supported(tail0->log2b, (int)tail0->S, (int)t0_nmax);
@@ -1211,8 +1197,7 @@ struct CrossfadeCore {
             // :72-73 on the lookahead step: each convolver's full
             // block runs its own launch of far / mid anchors and steps; then
             // the mix (:75-77)
-            static const bool split = [] { const char *e = getenv("FFTCONV_XF_SPLIT"); return e && atoi(e) > 0; }();
-            if (out_len == m && la_fuse_mix_allowed() && !split && a->la_t == b->la_t && a->la_seq == b->la_seq &&
+            if (out_len == m && la_fuse_mix_allowed() && a->la_t == b->la_t && a->la_seq == b->la_seq &&
                 a->la_all == b->la_all) {
                 // :72-77 in ONE launch: A's and B's anchors, and per channel
                 // one workgroup running A's and B's step (two chain waves)
@@ -1224,8 +1209,7 @@ struct CrossfadeCore {
                 pa.tw = a->tw.p;
                 pa.njobs = 2;
                 if (int r = a->la_fill(pa, s)) return r;
-                pa.laP2 = b->laP.p;
-                pa.laPm2 = b->laPm.p;
+                pa.laW2 = b->laW.p;
                 pa.la_mix = 3;
                 pa.mix = mix_args(dout, os, out_len);  // (buf_a / buf_b: the generic-step fallback)
                 HIP_TRY(launch_process_la(a->log2b, pa, (int)C, s));
@@ -1468,7 +1452,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 255 || variant < -1) return fail(FFTCONV_E_INVALID, "variant must be 0..255 (or -1 = auto)");
+    if (variant > 511 || variant < -1) return fail(FFTCONV_E_INVALID, "variant must be 0..511 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }

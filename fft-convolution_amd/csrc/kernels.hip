@@ -1742,35 +1742,40 @@ hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_
 }
 
 // Lookahead geometry policy: block sizes whose row is whole waves of float4
-// slots (128..512) and FDLs long enough that the far rows dominate.  A
+// slots (128..512) and FDLs long enough that the anchor levels dominate.  A
 // function of (B, S) only, never of the channel count.
 int la_parts(int log2b, int S) {
     if (log2b < 7 || log2b > 9) return 0;
     if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NOLA)) return 0;
-    if (S < LA_DF + 8) return 0;  // (channels whose active segments drop below DF + 2 step generically)
-    switch (log2b) {
-        case 7: return LaGeo<7>::WF;
-        case 8: return LaGeo<8>::WF;
-        default: return LaGeo<9>::WF;
+    if (S < 40) return 0;  // (channels whose active segments drop below D0 + 2 step generically)
+    return 1;
+}
+LaDims la_dims(int log2b, int S) {
+    LaDims d{};
+    d.nlv = la_nlv(S);
+    for (int lv = 1; lv <= 3; ++lv) d.per[lv - 1] = la_per(lv);
+    const int nsl = log2b >= 7 ? (1 << (log2b - 1)) / 64 : 1;  // LaGeo::NSL
+    d.wg[0] = log2b <= 8 ? 0 : 1;                               // LaStep::MIDIN: level 1 in the step workgroups
+    d.wg[1] = nsl * (LA_P2 / LA_JW);
+    d.wg[2] = d.nlv == 3 ? nsl * (LA_P3 / LA_JW) : 0;
+    d.pt = LA_PT;
+    d.per_all = LA_PER;
+    return d;
+}
+
+// anchor workgroups of a launch (ProcArgs::la_n): per level the scheduled
+// channels of [c0, C) -- all of them when la_all > 0 -- in whole XCD rounds
+// of 8 for the level 2/3 anchors (la_anchor_far)
+static void la_counts(ProcArgs &a, int log2b, int S, int C, bool all, bool mid_wg) {
+    const LaDims d = la_dims(log2b, S);
+    for (int lv = 1; lv <= 3; ++lv) {
+        const int P = d.per[lv - 1];
+        const int t0 = a.la_t % P;
+        const int n = all ? C - a.la_c0 : (C > t0 ? (C - t0 + P - 1) / P : 0);
+        if (lv == 1) a.la_n[0] = mid_wg ? n : 0;
+        else a.la_n[lv - 1] = (lv <= d.nlv) ? (n + 7) / 8 * 8 * d.wg[lv - 1] : 0;
     }
-}
-LaDims la_dims(int log2b) {
-    const int wg = log2b == 7 ? LaGeo<7>::WG_FAR : (log2b == 8 ? LaGeo<8>::WG_FAR : LaGeo<9>::WG_FAR);
-    static const bool midwg = [] { const char *e = getenv("FFTCONV_LA_MIDWG"); return e && atoi(e) > 0; }();
-    const bool mid = !midwg && (log2b == 7 ? LaStep<7>::MIDIN : (log2b == 8 ? LaStep<8>::MIDIN : LaStep<9>::MIDIN));
-    return LaDims{LA_DF, LA_DM, wg, mid ? 1 : 0};
-}
-static int la_probe() {  // timing experiments only: FFTCONV_LA_TIMING_PROBE (results are wrong)
-    static const int v = [] { const char *e = getenv("FFTCONV_LA_TIMING_PROBE"); return e ? atoi(e) : 0; }();
-    return v;
-}
-static int xf_steps_first() {  // crossfade (la_mix 3) grid order, FFTCONV_XF_STEPS_FIRST (tuning)
-    static const int v = [] { const char *e = getenv("FFTCONV_XF_STEPS_FIRST"); return e ? atoi(e) : 1; }();
-    return v;
-}
-static int la_steps_first() {
-    static const int v = [] { const char *e = getenv("FFTCONV_LA_STEPS_FIRST"); return e ? atoi(e) : 0; }();
-    return v;
+    a.la_nlv = d.nlv;
 }
 
 template <int LOG2B>
@@ -1786,12 +1791,12 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         const size_t lds0 = lsb > LG::anchor_bytes ? lsb : LG::anchor_bytes;
         const size_t lds1 = lds0 > gen ? lds0 : gen;
         const size_t lds = (lds1 + 15) / 16 * 16;
-        if (a.la_W != LG::WF || !a.laPm) return hipErrorInvalidValue;
-        if (xf3 && (a.njobs != 2 || !a.laP2 || !a.laPm2 || a.job[0].S != a.job[1].S || a.job[0].n != a.job[1].n ||
+        if (!a.laW) return hipErrorInvalidValue;
+        if (xf3 && (a.njobs != 2 || !a.laW2 || a.job[0].S != a.job[1].S || a.job[0].n != a.job[1].n ||
                     a.job[0].add0 || a.job[1].add0 || !a.mix.buf_a || !a.mix.buf_b))
             return hipErrorInvalidValue;
-        // the far-row streams: nontemporal once the whole H + FDL working set
-        // (re-read every D steps) exceeds the Infinity Cache
+        // the full-pass streams: nontemporal once the whole H + FDL working
+        // set exceeds the Infinity Cache
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
         const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
         auto kern = a.la_mix == 1   ? (ntl ? upols_la_kernel<LOG2B, true, 1> : upols_la_kernel<LOG2B, false, 1>)
@@ -1802,12 +1807,12 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         args.pipe = 0;
         args.lag = 0;
         args.la_channels = channels;
-        args.la_steps_first = xf3 ? xf_steps_first() : la_steps_first();
-        args.la_probe = la_probe();
-        if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) {
-            args.la_all = -1;  // no anchors: every eligible step sums all its rows
-            args.la_nfar = args.la_nmid = 0;
-        }
+        args.la_c0 = 0;
+        args.la_rebuild = 0;
+        args.la_t = a.la_t % LA_PER;
+        if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) args.la_all = -1;  // no anchors: every eligible step sums all its rows
+        la_counts(args, LOG2B, a.job[0].S, channels, args.la_all > 0, !LaStep<LOG2B>::MIDIN);
+        if (args.la_all < 0) args.la_n[0] = args.la_n[1] = args.la_n[2] = 0;
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
@@ -1815,8 +1820,7 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         const int nstep = (channels + nch - 1) / nch;
         if (a.la_mix == 2 && a.job[0].add0) return hipErrorInvalidValue;  // (the fused mix uses the add buffers' LDS)
         const int xwg = a.la_mix == 1 ? LA_XWG : 0;  // A's launch: the mix_value walk workgroups
-        const int nanch = xf3 && args.la_steps_first == 2 ? 2 * args.la_nfar + (2 * args.la_nmid + 7) / 8 * 8
-                                                          : (xf3 ? 2 : 1) * (args.la_nfar + args.la_nmid);
+        const int nanch = (xf3 ? 2 : 1) * (args.la_n[0] + args.la_n[1] + args.la_n[2]);
         hipLaunchKernelGGL(kern, dim3(nanch + nstep + xwg), dim3(LA_NT), lds, s, args);
         return hipGetLastError();
     }
@@ -1824,8 +1828,15 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
 
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;
-    if (a.njobs != (a.la_mix == 3 ? 2 : 1) || !a.laP) return hipErrorInvalidValue;
+    if (a.njobs != (a.la_mix == 3 ? 2 : 1) || !a.laW) return hipErrorInvalidValue;
     FFTCONV_DISPATCH(launch_la_t, log2b, a, channels, s)
+}
+
+int la_trace_grid(int log2b, int S, int channels) {
+    if (log2b < 7 || log2b > 9) return 0;
+    ProcArgs a{};
+    la_counts(a, log2b, S, channels, true, true);
+    return a.la_n[0] + a.la_n[1] + a.la_n[2] + channels + LA_XWG;
 }
 
 // ---------------------------------------------------------------------------
@@ -1833,16 +1844,14 @@ hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStre
 // :174-213 keeps the FDL but replaces H, so every partial-sum window is
 // stale).  Instead of the next process launch re-anchoring every channel on
 // its latency-critical path, the update enqueues this anchors-only launch:
-// each channel's far and mid windows, as the anchors of the previous launch
-// would have left them (la_anchor_state, la_rebuild), then the state words
-// pointing at them.  The next process launch is a steady-state launch.
+// each channel's windows of every level, as the anchors of the previous
+// launch would have left them (la_anchor_state, la_rebuild), then the state
+// words pointing at them.  The next process launch is a steady-state launch.
 // ---------------------------------------------------------------------------
 template <int LOG2B, bool NTL>
 __global__ __launch_bounds__(LA_NT, 4) void la_rebuild_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int b = (int)blockIdx.x;
-    if (b < a.la_nfar) la_anchor_far<LOG2B, NTL>(a, 0, b, smem);
-    else la_anchor_mid<LOG2B, NTL>(a, 0, b - a.la_nfar);
+    la_anchor<LOG2B, NTL>(a, 0, (int)blockIdx.x, smem);
 }
 
 // the state words of the rebuilt windows (same eligibility test as the
@@ -1855,8 +1864,7 @@ __global__ void la_rebuild_state_kernel(ProcArgs a) {
     if (!la_eligible<LOG2B>(st, a.job[0].n)) return;
     int nf = st.w & ~(LA_MASK | SEQ_MASK);  // (launch tag 0: no process launch wrote it)
     // (the anchors wrote the other window of each level: toggle its flag)
-    nf = (nf ^ FLAG_PWIN) | FLAG_LA | ((la_dnew(c, a, LA_DF) - 1) << LA_D_SHIFT);
-    nf = (nf ^ FLAG_PWINM) | FLAG_LAM | ((la_dnew(c, a, LA_DM) - 1) << LA_DM_SHIFT);
+    for (int lv = 1; lv <= a.la_nlv; ++lv) nf = (nf ^ la_flag_win(lv)) | la_flag_live(lv);
     a.job[0].state[c].w = nf;
 }
 
@@ -1867,8 +1875,7 @@ static hipError_t launch_rebuild_t(const ProcArgs &a, int channels, hipStream_t 
     } else {
         using LG = LaGeo<LOG2B>;
         constexpr size_t lds = (LG::anchor_bytes + 15) / 16 * 16 + 16;
-        if (a.la_W != LG::WF || !a.laPm || !a.laP || a.njobs != 1 || a.job[0].n != (1 << LOG2B))
-            return hipErrorInvalidValue;
+        if (!a.laW || a.njobs != 1 || a.job[0].n != (1 << LOG2B)) return hipErrorInvalidValue;
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
         const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
         auto kern = ntl ? la_rebuild_kernel<LOG2B, true> : la_rebuild_kernel<LOG2B, false>;
@@ -1877,16 +1884,15 @@ static hipError_t launch_rebuild_t(const ProcArgs &a, int channels, hipStream_t 
         args.la_all = 1;
         args.la_rebuild = 1;
         args.la_seq = 0;
-        args.la_probe = 0;
+        args.la_t = a.la_t % LA_PER;
         const int nch = channels - a.la_c0;
         if (nch <= 0) return hipSuccess;
-        args.la_nfar = (nch + 7) / 8 * 8 * LG::WG_FAR;
-        args.la_nmid = nch;
+        la_counts(args, LOG2B, a.job[0].S, channels, true, true);  // (level 1 in workgroups of its own)
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(kern, dim3(args.la_nfar + args.la_nmid), dim3(LA_NT), lds, s, args);
+        hipLaunchKernelGGL(kern, dim3(args.la_n[0] + args.la_n[1] + args.la_n[2]), dim3(LA_NT), lds, s, args);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
         hipLaunchKernelGGL(la_rebuild_state_kernel<LOG2B>, dim3((nch + 255) / 256), dim3(256), 0, s, args);
         return hipGetLastError();
@@ -1970,7 +1976,8 @@ hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hip
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 255); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 511); }
+bool tail0_defer_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_T0BLOCK); }
 bool la_fuse_mix_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_NOFMIX); }
 void set_pipeline_lag(int rows) { g_lag = rows < 0 ? -1 : rows; }
 int get_pipeline_lag() { return g_lag; }

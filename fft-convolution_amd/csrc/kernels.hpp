@@ -10,25 +10,22 @@ enum : int {
     FLAG_REV = 2,    // scan parity of the segment MAC (toggled per completed block)
     FLAG_PRE = 4,    // pre[] holds pre_multiplied of the block that starts at `current`
     FLAG_XSYNC = 8,  // crossfade pair: this FDL has always equalled its partner's
-    // lookahead (time-blocked FDL, see la.hpp): the far window of partial
-    // sums is live (FLAG_LA) in P window FLAG_PWIN, bits 8-12 = steps of it
-    // consumed, 13-17 = its length - 1; the mid window likewise (FLAG_LAM,
-    // FLAG_PWINM, bits 18-20, 21-23); bits 24-25 = the launch tag of the last
+    // lookahead (time-blocked FDL, see la.hpp): per anchor level lv = 1..3 the
+    // window of partial sums is live (FLAG_LA1 << 2(lv-1)) in window
+    // FLAG_PW1 << 2(lv-1) of the two; a step at launch t reads the row at
+    // position (t - 1 - c) mod P_lv.  Bits 24-25 = the launch tag of the last
     // process launch that wrote this state word
-    FLAG_LA = 16,
-    FLAG_PWIN = 32,
-    FLAG_LAM = 64,
-    FLAG_PWINM = 128,
-    LA_J_SHIFT = 8,
-    LA_D_SHIFT = 13,
-    LA_JM_SHIFT = 18,
-    LA_DM_SHIFT = 21,
+    FLAG_LA1 = 16,
+    FLAG_PW1 = 32,
+    FLAG_LA2 = 64,
+    FLAG_PW2 = 128,
+    FLAG_LA3 = 256,
+    FLAG_PW3 = 512,
     SEQ_SHIFT = 24,
-    // lookahead: pre[] holds the near rows' sum (rows D1..1) of the block
+    // lookahead: pre[] holds the near rows' sum (rows D0..1) of the block
     // that starts at `current`, left by the previous step (la.hpp)
     FLAG_NEAR = 1 << 26,
-    LA_MASK = FLAG_LA | FLAG_LAM | (31 << LA_J_SHIFT) | (31 << LA_D_SHIFT) | (7 << LA_JM_SHIFT) | (7 << LA_DM_SHIFT) |
-              FLAG_NEAR,
+    LA_MASK = FLAG_LA1 | FLAG_LA2 | FLAG_LA3 | FLAG_NEAR,
     SEQ_MASK = 3 << SEQ_SHIFT,
 };
 
@@ -38,6 +35,7 @@ enum : int {
     VARIANT_LAFULL = 32,  // lookahead launches without anchors: every step sums all rows itself (tests)
     VARIANT_NOFMIX = 64,  // crossfade on the lookahead step: stand-alone mix kernel instead of B's epilogue
     VARIANT_IRBLOCK = 128,  // IR transforms: one segment per workgroup (else one per wave, 64 <= B <= 1024)
+    VARIANT_T0BLOCK = 256,  // two-stage: tail0 per block (else deferred to the end of its period), read at create
     VARIANT_AUTO = 0x7fffffff
 };
 void set_variant(int v);
@@ -97,18 +95,13 @@ struct ProcArgs {
     int fuse_mix;          // crossfade pair launch: mix A and B into mix.out in-kernel
     CrossfadeMixArgs mix;  // (buf_a / buf_b unused then)
     // lookahead launch (launch_process_la; job[0] only)
-    float2 *laP;           // [C][2 windows][LA_DF][la_W][B] far-row partial sums
-    float2 *laPm;          // [C][2 windows][LA_DM][B] mid-row partial sums
-    float2 *laP2, *laPm2;  // job[1]'s windows (la_mix 3: the crossfade's B in the same launch)
-    int la_W;              // far parts (partial rows per step)
-    int la_nfar;           // far anchor workgroups at the front of the grid
-    int la_nmid;           // mid anchor workgroups after them
+    float2 *laW;           // [C][2 windows][LA_PT][B]: the partial-sum windows of levels 1..3
+    float2 *laW2;          // job[1]'s windows (la_mix 3: the crossfade's B in the same launch)
+    int la_n[3];           // anchor workgroups of levels 1..3 (grid: level 3, 2, 1, then the steps)
+    int la_nlv;            // anchor levels: 3, or 2 when no FDL row reaches level 3 (S <= LA_R2 + 1)
     int la_all;            // 1: every channel is scheduled for anchors (entry launch); -1: none is
-    int la_t;              // launch counter mod LA_DF*LA_DM: channel c anchors at period P when (c - t) % P == 0
+    int la_t;              // launch counter mod LA_PER: channel c anchors at period P when (c - t) % P == 0
     int la_seq;            // 1 or 2, alternating per lookahead launch; 0 in every other launch
-    int la_steps_first;    // grid order: step workgroups before the anchors (tuning)
-    int la_probe;          // timing probe only (wrong results): 1 = anchors idle, 2 = steps idle,
-                           // 3 = far anchors only, 4 = mid anchors only
     int la_channels;       // channels of the batch (step workgroups cover LaStep::NCH each)
     // crossfade on the lookahead step (CrossfadeConvolver::process :72-77):
     // 1 = A's launch also writes this call's per-sample mix selectors to mix_tab;
@@ -184,14 +177,21 @@ bool pair_supported(int log2b, int S);
 hipError_t launch_process_pair(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hipStream_t s);
 size_t process_lds_bytes(int log2b);
-// lookahead: far parts (partial rows per step) for this geometry, 0 = not used
+// lookahead: 1 if this geometry takes the lookahead step, else 0
 int la_parts(int log2b, int S);
+// the lookahead launch shape of a geometry (la.hpp): anchor levels, the
+// workgroups per anchor of each level (level 1: 0 = run by the step
+// workgroups), and the periods
 struct LaDims {
-    int DF, DM;       // far / mid periods
-    int wg_far;       // workgroups per far anchor
-    int mid_in_step;  // the step workgroups run the mid anchors (no mid workgroups)
+    int nlv;
+    int per[3];
+    int wg[3];
+    int pt;           // window rows per channel and window (all levels)
+    int per_all;      // the stagger clock's modulus
 };
-LaDims la_dims(int log2b);
+LaDims la_dims(int log2b, int S);
+// launch timeline records per lookahead launch (FFTCONV_LA_TRACE): the largest grid
+int la_trace_grid(int log2b, int S, int channels);
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 // every far and mid window of channels [a.la_c0, channels) rebuilt from the
 // current H and FDL (anchors only), then their state words pointed at them
@@ -217,6 +217,7 @@ struct Tail0Args {
     int nmax;              // row pitch of xs / ys in blocks
 };
 bool tail0_defer_supported(int log2b, int act, int nmax);
+bool tail0_defer_allowed();  // VARIANT_T0BLOCK unset
 hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s);
 
 constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)

@@ -8,34 +8,39 @@
 // where X_b is the spectrum of block b (FDL row (current + age) % act).  Every
 // step re-reads all act rows of H and of the FDL: 16 B per bin-row, 773 KB
 // per channel-block at cfg2.  But a row i only meets blocks at least i steps
-// old, so its terms for the next j < i steps are known now.  The rows split in
-// three levels by that horizon:
-//   near rows  1..D1       summed by each step itself;
-//   mid rows   D1+1..DF    summed by a *mid anchor* every DM = D1 steps, for
-//                          the DM steps after it (X ages >= 1 at the anchor);
-//   far rows   DF+1..act-1 summed by a *far anchor* every DF steps, for the
-//                          DF steps after it.
-// (D1 = DM = 4, DF = 32: r1j A/B, DF = 16 was 9.5 % slower at cfg2.)
+// old, so its terms for the next j < i steps are known now.  The rows split
+// into a near level and three anchor levels by that horizon:
+//   near rows 1..D0          summed by each step itself;
+//   level 1  rows D0+1..R1   summed by an anchor every P1 <= D0 steps for the
+//                            P1 steps after it (X ages >= 1 at the anchor);
+//   level 2  rows R1+1..R2   every P2 <= R1 steps, for the P2 steps after it;
+//   level 3  rows R2+1..     every P3 <= R2 steps, for the P3 steps after it.
+// (D0 = P1 = 4, R1 = P2 = 16, R2 = P3 = 64: geometric periods.  Against the
+// three levels of round 2 -- near 1..5, 6..32 every 5, 33.. every 32 -- the
+// row transfers per cfg2 channel-block drop from 40.3 to 36.5 and the
+// longest walks from 27 (in-step) / 39 (far) rows to 12 / 31.)
 // An anchor walks its rows once, keeping a window of X rows in registers, and
-// leaves one partial-sum row per future step (P windows in HBM).  Per channel-
-// block the far rows then cost 16 B (S - DF) / DF per bin instead of 16 B S,
-// the mid rows 16 B (DF - D1) / DM, the near rows 16 B D1 (hot in the
-// Infinity Cache).  The step stays zero-latency: step s needs nothing after
-// block s.
+// leaves one partial-sum row per future step (the level's window in HBM).
+// Per channel-block level L costs 16 B (2 n_L + P_L - 1) / (2 P_L) per bin
+// for its n_L rows, plus one window row written and one read.  The step stays
+// zero-latency: step s needs nothing after block s.
 //
 // Anchors are staggered over channels (channel c anchors at level L when
-// (c - t) % period_L == 0, t = launch counter), so every launch carries C/DF
-// far and C/DM mid anchors and the per-launch bytes are even.  Anchor and step
+// (c - t) % P_L == 0, t = launch counter), so every launch carries C/P_L
+// anchors of each level and the per-launch bytes are even.  Anchor and step
 // workgroups of one launch touch disjoint memory: an anchor reads FDL ages
-// >= 1 (the step writes age 0) and writes the other P window of its level
-// (two per channel and level).
+// >= 1 (the step writes age 0) and writes the other window of its level (two
+// per channel and level).  A window row is stored at the position of the
+// step it serves: the step of launch t reads row (t - 1 - c) mod P_L, so an
+// anchor that opens a short window (entry, rebuild: up to the channel's next
+// stagger slot) writes the tail of the window and no step counter is kept.
 //
 // Summation order (canonical, phase independent).  Each level is a fixed set
-// of sequential chains: near rows D1..1; mid rows DF..D1+1; far rows [DF+1,
-// act) in NG fixed groups (even groups descending, odd ascending, so that
-// neighbouring groups read their shared window rows at the same time) combined
-// sequentially within a far part and then over the parts.  Then
-//     pre = near + (mid + far),   conv = pre + H[0] (.) X_s   (slot_mac, :256-261).
+// of sequential chains: near rows D0..1; level 1 rows R1..D0+1; levels 2 and
+// 3 in NG fixed groups (even groups descending, odd ascending, so that
+// neighbouring groups read their shared window rows at the same time)
+// combined in group order.  Then
+//     pre = near + (W1 + (W2 + W3)),   conv = pre + H[0] (.) X_s  (slot_mac, :256-261).
 // An anchor's accumulator for step a+j visits exactly the rows and blocks the
 // step a+j would, in the same order, so a step served from windows and a step
 // that sums everything itself (entry, after update / reset / partial calls,
@@ -44,38 +49,36 @@
 #pragma once
 // (no namespace of its own: included inside namespace fftconv)
 
-constexpr int LA_D1 = 5;             // near rows, summed by the step
-constexpr int LA_DM = 5;             // mid period / window (<= LA_D1)
-constexpr int LA_DF = 32;            // far period / window; mid rows are D1+1..DF
-constexpr int LA_JW = 8;             // far window steps per laneset (register window)
-constexpr int LA_U = 2;              // anchor: H / X rows in flight per lane
-constexpr int LA_UF = 2;             // far anchor: H / X rows in flight per lane
-constexpr int LA_UM = 2;             // mid anchor: H / X rows in flight per lane
-constexpr int LA_NT = 256;           // threads per workgroup (anchor and step roles)
-// LA_HW = 1: far anchors walk their rows in half-wave lanesets (32 lanes = 64
-// bins of a row), 8 far-row groups per workgroup instead of 4 full-wave ones,
-// so each walk is half as long and one workgroup still combines every group
-// in LDS into one window row per step.  Measured (r2g, cfg2, same-process
-// A/B): the far walks end at 12.5 instead of 15.5 us of the launch, but their
-// doubled request rate delays the steps' loads (helpers' pre 11.9 vs 8.7 us)
-// and the launch is slower: 21.60 vs 18.62 us.  The launch is bound by its
-// bytes in flight, not by the far chain alone; kept as an option.
-constexpr int LA_HW = 0;
-// far-row groups per anchor: 4 (one full-wave laneset each; a far anchor
-// workgroup's four waves), 8 from B = LA_NG8_B on -- two far parts, i.e. two
-// window rows per step, and twice the far workgroups, each walking half the
-// rows.  Measured at cfg5 (r2t, B = 512): the far walks end sooner, but the
-// launch is bound by its bytes, not by the walks' slots: 45.8 vs 41.7 us per
-// step, so the default keeps 4 groups (LA_NG8_B beyond the lookahead range)
-#ifndef FFTCONV_LA_NG8_B
-#define FFTCONV_LA_NG8_B 1024
-#endif
-constexpr int LA_NG8_B = FFTCONV_LA_NG8_B;
-template <int LOG2B>
-__host__ __device__ constexpr int la_ng() { return LA_HW || (1 << LOG2B) >= LA_NG8_B ? 8 : 4; }
-constexpr int LA_CU = 8;             // full-pass chain: rows in flight per lane
-constexpr int LA_OOB = 0x7ffffff0;   // a buffer voffset past every stream's range
-static_assert(LA_DM <= LA_D1 && LA_DM <= 8 && LA_DF <= 32 && LA_DF % LA_JW == 0, "lookahead levels (state word fields)");
+constexpr int LA_D0 = 4;                     // near rows 1..D0, summed by the step
+constexpr int LA_P1 = 4, LA_R1 = 16;         // level 1: rows D0+1..R1, period P1
+constexpr int LA_P2 = 16, LA_R2 = 64;        // level 2: rows R1+1..R2, period P2
+constexpr int LA_P3 = 64;                    // level 3: rows R2+1..act-1, period P3
+constexpr int LA_PT = LA_P1 + LA_P2 + LA_P3;  // window rows per channel and window
+constexpr int LA_PER = 64;                   // stagger clock modulus (every period divides it)
+constexpr int LA_JW = 8;                     // far-style window steps per workgroup (register window)
+constexpr int LA_U = 2;                      // anchor: H / X rows in flight per lane
+constexpr int LA_UF = 2;                     // level 2/3 anchors: H / X rows in flight per lane
+constexpr int LA_UM = 2;                     // level 1 anchors: H / X rows in flight per lane
+constexpr int LA_NT = 256;                   // threads per workgroup (anchor and step roles)
+constexpr int LA_NG = 4;                     // row groups of a level 2/3 anchor (one wave each)
+constexpr int LA_CU = 8;                     // full-pass chain: rows in flight per lane
+constexpr int LA_OOB = 0x7ffffff0;           // a buffer voffset past every stream's range
+static_assert(LA_P1 <= LA_D0 && LA_P2 <= LA_R1 && LA_P3 <= LA_R2, "a level's rows are older than its window");
+static_assert(LA_PER % LA_P1 == 0 && LA_PER % LA_P2 == 0 && LA_PER % LA_P3 == 0, "stagger clock");
+static_assert(LA_P2 % LA_JW == 0 && LA_P3 % LA_JW == 0 && LA_P1 <= 8, "window slices");
+
+// level lv (1..3): period, first row, end of its rows for an FDL of act
+// segments, offset of its window rows
+__host__ __device__ constexpr int la_per(int lv) { return lv == 1 ? LA_P1 : (lv == 2 ? LA_P2 : LA_P3); }
+__host__ __device__ constexpr int la_lo(int lv) { return lv == 1 ? LA_D0 + 1 : (lv == 2 ? LA_R1 + 1 : LA_R2 + 1); }
+__host__ __device__ constexpr int la_hi(int lv, int act) {
+    return lv == 1 ? (act < LA_R1 + 1 ? act : LA_R1 + 1) : (lv == 2 ? (act < LA_R2 + 1 ? act : LA_R2 + 1) : act);
+}
+__host__ __device__ constexpr int la_off(int lv) { return lv == 1 ? 0 : (lv == 2 ? LA_P1 : LA_P1 + LA_P2); }
+__host__ __device__ constexpr int la_flag_live(int lv) { return FLAG_LA1 << (2 * (lv - 1)); }
+__host__ __device__ constexpr int la_flag_win(int lv) { return FLAG_PW1 << (2 * (lv - 1)); }
+// anchor levels of a geometry: level 3 only when some FDL row reaches it
+__host__ __device__ constexpr int la_nlv(int S) { return S > LA_R2 + 1 ? 3 : 2; }
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -107,22 +110,15 @@ struct LaAcc {
     __device__ __forceinline__ float4 get() const { return make_float4(a01.x, a01.y, a23.x, a23.y); }
 };
 
-// state word fields (kernels.hpp): far window {FLAG_LA, FLAG_PWIN, j, d-1},
-// mid window {FLAG_LAM, FLAG_PWINM, jm, dm-1}
-__device__ __forceinline__ int la_jf(int w) { return (w >> LA_J_SHIFT) & 31; }
-__device__ __forceinline__ int la_df(int w) { return ((w >> LA_D_SHIFT) & 31) + 1; }
-__device__ __forceinline__ int la_jm(int w) { return (w >> LA_JM_SHIFT) & 7; }
-__device__ __forceinline__ int la_dm(int w) { return ((w >> LA_DM_SHIFT) & 7) + 1; }
-__device__ __forceinline__ bool la_far_live(int w) { return (w & FLAG_LA) && la_jf(w) < la_df(w); }
-__device__ __forceinline__ bool la_mid_live(int w) { return (w & FLAG_LAM) && la_jm(w) < la_dm(w); }
+__device__ __forceinline__ bool la_live(int w, int lv) { return (w & la_flag_live(lv)) != 0; }
 
 // the lookahead step applies: one whole block from an empty input buffer, at
-// least one far row
+// least one level-1 row
 template <int LOG2B>
 __device__ __forceinline__ bool la_eligible(int4 st, int n) {
-    return n == (1 << LOG2B) && st.z == 0 && !(st.w & FLAG_INBUF) && st.y >= LA_DF + 2 && st.x < st.y;
+    return n == (1 << LOG2B) && st.z == 0 && !(st.w & FLAG_INBUF) && st.y >= LA_D0 + 2 && st.x < st.y;
 }
-// stagger phase of channel c at level period P (la_t = launch counter mod DF*DM)
+// stagger phase of channel c at level period P (la_t = launch counter mod LA_PER)
 __device__ __forceinline__ int la_phase(int c, const ProcArgs &a, int P) {
     const int r = (c - a.la_t) % P;
     return r < 0 ? r + P : r;
@@ -135,41 +131,35 @@ __device__ __forceinline__ int la_dnew(int c, const ProcArgs &a, int P) {
     const int r = la_phase(c, a, P);
     return r == 0 ? P : r;
 }
-// mid window split over L lanesets: ceil(DM / L) steps each; the last laneset's
-// run is shifted back to end at step DM (no step past the window: its rows
-// would meet blocks not yet written) and stores only the steps it owns
-__host__ __device__ constexpr int la_mid_per(int L) { return (LA_DM + (L < LA_DM ? L : LA_DM) - 1) / (L < LA_DM ? L : LA_DM); }
-__device__ __forceinline__ int la_mid_j0(int l, int JM) { return min(l * JM, LA_DM - JM); }
-// far-row group g walks descending (LA_HW: every group, so the two groups of a
-// wave share their walk direction) or ascending for odd g (full-wave groups:
-// neighbouring groups then read their shared X rows at the same time)
-__host__ __device__ constexpr bool la_asc(int g) { return LA_HW ? false : (g & 1) != 0; }
-// far-row group g of NG: rows [lo, hi) of [DF+1, act)
-template <int LOG2B>
-__device__ __forceinline__ void la_group(int g, int act, int &lo, int &hi) {
-    constexpr int NG = la_ng<LOG2B>();
-    const int nf = act - LA_DF - 1;
-    lo = LA_DF + 1 + (g * nf) / NG;
-    hi = LA_DF + 1 + ((g + 1) * nf) / NG;
+// the window row the step of this launch reads: (t - 1 - c) mod P
+__device__ __forceinline__ int la_pos(int c, const ProcArgs &a, int P) {
+    const int r = (a.la_t - 1 - c) % P;
+    return r < 0 ? r + P : r;
 }
-// window rows: far P[c][win][j][w] (w < la_W parts), mid P[c][win][j]
-__device__ __forceinline__ float4 *la_pf(const ProcArgs &a, int jb, size_t c, int win, int j, int w, int B) {
+// level-1 window split over L lanesets: ceil(P1 / L) steps each; the last
+// laneset's run is shifted back to end at step P1 (no step past the window:
+// its rows would meet blocks not yet written) and stores only the steps it owns
+__host__ __device__ constexpr int la_mid_per(int L) { return (LA_P1 + (L < LA_P1 ? L : LA_P1) - 1) / (L < LA_P1 ? L : LA_P1); }
+__device__ __forceinline__ int la_mid_j0(int l, int JM) { return min(l * JM, LA_P1 - JM); }
+// row group g (of NG) of level lv walks descending, or ascending for odd g
+// (neighbouring groups then read their shared X rows at the same time)
+__host__ __device__ constexpr bool la_asc(int g) { return (g & 1) != 0; }
+// level lv's row group g of LA_NG: rows [lo, hi) (empty when act is short)
+__device__ __forceinline__ void la_group(int lv, int g, int act, int &lo, int &hi) {
+    const int l0 = la_lo(lv), h0 = la_hi(lv, act);
+    const int nf = h0 > l0 ? h0 - l0 : 0;
+    lo = l0 + (g * nf) / LA_NG;
+    hi = l0 + ((g + 1) * nf) / LA_NG;
+}
+// window row `pos` of level lv: W[c][win][off(lv) + pos]
+__device__ __forceinline__ float4 *la_win(const ProcArgs &a, int jb, size_t c, int win, int lv, int pos, int B) {
 #ifdef FFTCONV_DEBUG_BOUNDS
-    if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && j >= 0 && j < LA_DF && w >= 0 && w < a.la_W)) {
-        printf("BOUNDS la_pf blk %d c %d win %d j %d w %d\n", (int)blockIdx.x, (int)c, win, j, w);
-        c = 0; win = 0; j = 0; w = 0;
+    if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && lv >= 1 && lv <= 3 && pos >= 0 && pos < la_per(lv))) {
+        printf("BOUNDS la_win blk %d c %d win %d lv %d pos %d\n", (int)blockIdx.x, (int)c, win, lv, pos);
+        c = 0; win = 0; lv = 1; pos = 0;
     }
 #endif
-    return reinterpret_cast<float4 *>((jb ? a.laP2 : a.laP) + ((((c * 2 + win) * LA_DF + j) * (size_t)a.la_W + w) * (size_t)B));
-}
-__device__ __forceinline__ float4 *la_pm(const ProcArgs &a, int jb, size_t c, int win, int j, int B) {
-#ifdef FFTCONV_DEBUG_BOUNDS
-    if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && j >= 0 && j < LA_DM)) {
-        printf("BOUNDS la_pm blk %d c %d win %d j %d\n", (int)blockIdx.x, (int)c, win, j);
-        c = 0; win = 0; j = 0;
-    }
-#endif
-    return reinterpret_cast<float4 *>((jb ? a.laPm2 : a.laPm) + (((c * 2 + win) * LA_DM + j) * (size_t)B));
+    return reinterpret_cast<float4 *>((jb ? a.laW2 : a.laW) + (((c * 2 + win) * LA_PT + la_off(lv) + pos) * (size_t)B));
 }
 
 // ---------------------------------------------------------------------------
@@ -177,6 +167,7 @@ __device__ __forceinline__ float4 *la_pm(const ProcArgs &a, int jb, size_t c, in
 // j = j0+1 .. j0+JW: acc[jj] += H[i] (.) X(age i - j0 - 1 - jj at the anchor),
 // rows in the chain's order.  X rows live in a register ring indexed by the
 // walk position e; each row of H and of the FDL is loaded once, LA_U ahead.
+// (Callers pass hi > lo.)
 // ---------------------------------------------------------------------------
 template <int LOG2B, bool ASC, bool NTL, int JW, int U = LA_U>
 __device__ __forceinline__ void la_walk(LaAcc (&acc)[JW], const RowStream &hs, const RowStream &xs, int voff,
@@ -220,48 +211,6 @@ __device__ __forceinline__ void la_walk(LaAcc (&acc)[JW], const RowStream &hs, c
     }
 }
 
-// The far walk of a half-wave laneset (LA_HW): rows [lo, hi) descending, with
-// lo / hi per lane (a wave holds two lanesets, i.e. two far-row groups), so
-// every offset is a per-lane voffset; `nmax` = the wave's longer walk, the
-// shorter one idles its last row.  Same accumulator order as la_walk
-// (descending): acc[jj] += H[i] (.) X(age i - j0 - 1 - jj at the anchor).
-template <int LOG2B, int JW, int U>
-__device__ __forceinline__ void la_walk_lane(LaAcc (&acc)[JW], const RowStream &hs, const RowStream &xs, int voff,
-                                             bool z0, int lo, int hi, int nmax, int j0, int cur, int act) {
-    constexpr int ROWB = (1 << LOG2B) * (int)sizeof(float2);
-    constexpr int RS = JW + U;
-    constexpr int UNR = RS % U == 0 ? RS : RS * U;
-    const int n = hi - lo;
-    const int ne = n + JW - 1;
-    auto xo = [&](int e) {  // X ring entry e: age hi - 2 - j0 - e >= 1
-        int r = cur + hi - 2 - j0 - e;
-        if (r >= act) r -= act;
-        return e < ne ? voff + r * ROWB : LA_OOB;
-    };
-    auto ho = [&](int k) { return k < n ? voff + (hi - 1 - k) * ROWB : LA_OOB; };
-    float4 xr[RS], hr[U];
-#pragma unroll
-    for (int e = 0; e < RS - 1; ++e) xr[e] = xs.ld4<false>(xo(e), 0);
-#pragma unroll
-    for (int k = 0; k < U; ++k) hr[k] = hs.ld4<false>(ho(k), 0);
-#pragma nounroll
-    for (int k0 = 0; k0 < nmax; k0 += UNR) {
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const int k = k0 + u;
-            if (k >= nmax) break;
-            if (k < n) {
-                const LaH h = la_ops(hr[u % U], z0);
-#pragma unroll
-                for (int jj = 0; jj < JW; ++jj) acc[jj].mac(h, xr[(u + jj) % RS]);
-            }
-            hr[u % U] = hs.ld4<false>(ho(k + U), 0);
-            xr[(u + RS - 1) % RS] = xs.ld4<false>(xo(k + RS - 1), 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
 // One chain for the current step (X age i), the same rows in the same order
 // as an anchor's accumulators.
 template <int LOG2B, bool ASC, bool NTL>
@@ -290,23 +239,20 @@ __device__ __forceinline__ void la_chain(LaAcc &acc, const RowStream &hs, const 
 template <int LOG2B>
 struct LaGeo {
     static constexpr int B = 1 << LOG2B, F = B / 2, LPW = LA_NT / F;  // lanesets of F lanes per workgroup
-    // far anchor workgroup: one bin slice of FS lanes (bins are independent),
-    // GPW far groups (one wave-sized laneset each) of one window slice of JW
-    // steps, combined in LDS; one anchor = NSL slices x WF parts x (DF / JW)
-    // window slices, XCD-aligned (see la_anchor_far)
-    static constexpr int FW = LA_HW ? 32 : 64;                      // lanes per far laneset
-    static constexpr int FS = F < FW ? F : FW, NSL = F / FS, LPF = LA_NT / FS;
-    static constexpr int NG = la_ng<LOG2B>();
-    static constexpr int GPW = LPF < NG ? LPF : NG;
-    static constexpr int WF = NG / GPW;                             // far parts (P rows per step)
-    static_assert(NG % GPW == 0, "far groups must fill whole parts");
-    static constexpr int WG_FAR = NSL * WF * (LA_DF / LA_JW);       // workgroups per far anchor
-    static constexpr int JM = la_mid_per(LPW);                      // mid window steps per laneset
-    static constexpr size_t anchor_bytes = (size_t)(GPW - 1) * LA_JW * FS * 16;
+    // level 2/3 anchor workgroup: one bin slice of FS lanes (bins are
+    // independent), the NG row groups (one wave-sized laneset each) of one
+    // window slice of JW steps, combined in LDS into one window row per step;
+    // one anchor = NSL bin slices x (P / JW) window slices, XCD-aligned (see
+    // la_anchor_far)
+    static constexpr int FS = F < 64 ? F : 64, NSL = F / FS, LPF = LA_NT / FS;
+    static_assert(LPF == LA_NG, "one row group per wave-sized laneset");
+    static constexpr int WG2 = NSL * (LA_P2 / LA_JW), WG3 = NSL * (LA_P3 / LA_JW);  // workgroups per anchor
+    static constexpr int JM = la_mid_per(LPW);                  // level-1 window steps per laneset
+    static constexpr size_t anchor_bytes = (size_t)(LA_NG - 1) * LA_JW * FS * 16;
 };
 
-// the anchor's view of channel c: its ring position, window and length, or
-// false if this launch opens no window of the level (period P) at c.
+// the anchor's view of channel c at level lv: its ring position, window and
+// length, or false if this launch opens no window of the level at c.
 //
 // Memory-model assumption (the one shared word of a launch).  The channel's
 // step workgroup stores state[c] once, as ONE 16-byte store from one lane
@@ -322,15 +268,16 @@ struct LaGeo {
 // Nothing else of the step is read by an anchor (FDL ages >= 1 only, the
 // other window of each level).
 template <int LOG2B>
-__device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c, int P, int &cur, int &act, int &win,
+__device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c, int lv, int &cur, int &act, int &win,
                                                 int &d) {
     const ProcJob &J = a.job[jb];
-    DBG_CHECK(c >= 0 && c < a.la_channels, "anchor state blk %d c %d P %d\n", (int)blockIdx.x, c, P);
+    DBG_CHECK(c >= 0 && c < a.la_channels, "anchor state blk %d c %d lv %d\n", (int)blockIdx.x, c, lv);
     const int4 st = J.state[c];
     const int sx = __builtin_amdgcn_readfirstlane(st.x), sy = __builtin_amdgcn_readfirstlane(st.y);
     const int sz = __builtin_amdgcn_readfirstlane(st.z), sw = __builtin_amdgcn_readfirstlane(st.w);
-    const bool far = P == LA_DF;
+    const int pw = la_flag_win(lv);
     act = sy;
+    d = la_dnew(c, a, la_per(lv));
     if (a.la_rebuild) {
         // window rebuild (no steps in this launch): the window an anchor of
         // the previous launch would have opened, i.e. as after that launch's
@@ -338,58 +285,51 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c
         // row i meets FDL row (sx + i) % act = age i - 1 from sx + 1
         if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return false;
         cur = sx + 1 == act ? 0 : sx + 1;
-        win = (sw & (far ? FLAG_PWIN : FLAG_PWINM)) ? 0 : 1;
-        d = la_dnew(c, a, P);
+        win = (sw & pw) ? 0 : 1;
         return true;
     }
     if (((sw & SEQ_MASK) >> SEQ_SHIFT) == a.la_seq) {
         // this launch's step has already stored the channel's state: it
-        // opened a window iff the state says so (j = 0)
-        if (far ? (!(sw & FLAG_LA) || la_jf(sw) != 0) : (!(sw & FLAG_LAM) || la_jm(sw) != 0)) return false;
+        // opened the window (this channel is scheduled) iff the level is live
+        if (!la_live(sw, lv)) return false;
         cur = sx + 1 == act ? 0 : sx + 1;
-        win = (sw & (far ? FLAG_PWIN : FLAG_PWINM)) ? 1 : 0;
-        d = far ? la_df(sw) : la_dm(sw);
+        win = (sw & pw) ? 1 : 0;
     } else {
         if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return false;
         cur = sx;
-        win = (sw & (far ? FLAG_PWIN : FLAG_PWINM)) ? 0 : 1;
-        d = la_dnew(c, a, P);
+        win = (sw & pw) ? 0 : 1;
     }
     return true;
 }
 
 // ---------------------------------------------------------------------------
-// Far anchor workgroup b: part w, window half(s) of channel c's far anchor
-// (groups w*GPW .. +GPW-1), combined in group order and stored as window rows
-// Pf[win][j][w].
+// Level LV (2 or 3) anchor workgroup b: bin slice and window slice of one
+// channel's anchor; the NG row groups (one per wave) combined in group order
+// and stored as one window row per step.
 // ---------------------------------------------------------------------------
-template <int LOG2B, bool NTL>
+template <int LOG2B, int LV, bool NTL>
 __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, unsigned char *smem) {
     using LG = LaGeo<LOG2B>;
-    constexpr int B = LG::B, GPW = LG::GPW;
+    constexpr int B = LG::B, P = la_per(LV), FS = LG::FS, NSL = LG::NSL;
+    constexpr int WGA = NSL * (P / LA_JW);
     const ProcJob &J = a.job[jb];
-    // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so the
-    // WG_FAR workgroups of one anchor sit 8 apart -- on one XCD, whose L2
-    // then serves the rows the window halves and neighbouring groups share
+    // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so the WGA
+    // workgroups of one anchor sit 8 apart -- on one XCD, whose L2 then
+    // serves the rows the window slices and neighbouring groups share
     const int x = b & 7, y = b >> 3;
-    const int ci = (y / LG::WG_FAR) * 8 + x, r = y % LG::WG_FAR;
-    const int c = a.la_all > 0 ? a.la_c0 + ci : (a.la_t % LA_DF) + LA_DF * ci;
+    const int ci = (y / WGA) * 8 + x, r = y % WGA;
+    const int c = a.la_all > 0 ? a.la_c0 + ci : (a.la_t % P) + P * ci;
     if (c >= a.la_channels) return;  // (padding of the last XCD round)
     int cur, act, win, d;
-    if (!la_anchor_state<LOG2B>(a, jb, c, LA_DF, cur, act, win, d)) return;
-    if ((r / (LG::NSL * LG::WF)) * LA_JW >= d) return;  // a window slice wholly past the window
+    if (!la_anchor_state<LOG2B>(a, jb, c, LV, cur, act, win, d)) return;
+    const int h = r / NSL;                   // window slice: steps h*JW .. h*JW+JW-1
+    if (h * LA_JW >= d) return;              // (wholly past the window)
 
-    constexpr int FS = LG::FS, NSL = LG::NSL;
     const int tid = threadIdx.x;
-    // (LA_HW: a laneset is half a wave, its index is per lane)
-    const int l = LA_HW ? tid / FS : __builtin_amdgcn_readfirstlane(tid / FS), fl = tid % FS;
-    if (!LA_HW && l >= GPW) return;                    // (more lanesets than groups)
-    const int f = (r % NSL) * FS + fl;                 // bin slice
-    const int w = (r / NSL) % LG::WF;                  // part
-    const int h = r / (NSL * LG::WF);                  // window slice: steps h*JW+1 .. h*JW+JW
-    const int g = w * GPW + l;
+    const int l = __builtin_amdgcn_readfirstlane(tid / FS), fl = tid % FS;
+    const int f = (r % NSL) * FS + fl;       // bin slice
     int lo, hi;
-    la_group<LOG2B>(g, act, lo, hi);
+    la_group(LV, l, act, lo, hi);
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
     const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
@@ -398,68 +338,68 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
     for (int j = 0; j < LA_JW; ++j) acc[j].zero();
     // (plain loads: the nontemporal policy streamed no faster here and cost the
     // step workgroups' cache-resident near rows ~8 % of the launch, r1i_la15_ab)
-    if constexpr (LA_HW) {
-        static_assert(LG::FS * 2 == 64 && LG::WF == 1, "half-wave far lanesets");
-        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-        int lo0, hi0, lo1, hi1;  // the wave's two groups
-        la_group<LOG2B>(2 * wv, act, lo0, hi0);
-        la_group<LOG2B>(2 * wv + 1, act, lo1, hi1);
-        const int nmax = max(hi0 - lo0, hi1 - lo1);
-        if (nmax > 0) la_walk_lane<LOG2B, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, nmax, h * LA_JW, cur, act);
-    } else if (hi > lo) {
-        if (la_asc(g)) la_walk<LOG2B, true, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+    if (hi > lo) {
+        if (la_asc(l)) la_walk<LOG2B, true, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
         else la_walk<LOG2B, false, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
     }
-    if constexpr (GPW > 1) {
-        float4 *red = reinterpret_cast<float4 *>(smem);  // [GPW-1][JW][FS]
-        if (l > 0) {
+    float4 *red = reinterpret_cast<float4 *>(smem);  // [NG-1][JW][FS]
+    if (l > 0) {
 #pragma unroll
-            for (int j = 0; j < LA_JW; ++j) red[((l - 1) * LA_JW + j) * FS + fl] = acc[j].get();
-        }
-        __syncthreads();
-        if (l == 0) {
+        for (int j = 0; j < LA_JW; ++j) red[((l - 1) * LA_JW + j) * FS + fl] = acc[j].get();
+    }
+    __syncthreads();
+    if (l == 0) {
 #pragma unroll
-            for (int j = 0; j < LA_JW; ++j) {
-                if (h * LA_JW + j < d) {
-                    float4 p = acc[j].get();
+        for (int j = 0; j < LA_JW; ++j) {
+            const int jj = h * LA_JW + j;
+            if (jj < d) {
+                float4 p = acc[j].get();
 #pragma unroll
-                    for (int q = 1; q < GPW; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * FS + fl]);
-                    la_pf(a, jb, c, win, h * LA_JW + j, w, B)[f] = p;
-                }
+                for (int q = 1; q < LA_NG; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * FS + fl]);
+                la_win(a, jb, c, win, LV, P - d + jj, B)[f] = p;
             }
         }
-    } else {
-#pragma unroll
-        for (int j = 0; j < LA_JW; ++j)
-            if (h * LA_JW + j < d) la_pf(a, jb, c, win, h * LA_JW + j, w, B)[f] = acc[j].get();
     }
 }
 
-// Mid anchor workgroup b: channel c's mid rows DF..D1+1 (one descending chain
-// per window step), the window steps split over the lanesets.
-template <int LOG2B, bool NTL>
-__device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int jb, int b) {
-    using LG = LaGeo<LOG2B>;
-    constexpr int B = LG::B, F = LG::F, JM = LG::JM;
+// Level-1 anchor: channel c's rows R1..D0+1 (one descending chain per window
+// step), the window steps split over the lanesets of l0 .. (l0 + L) with
+// threads [t0, t0 + L*F).  Used by the level-1 anchor workgroups (B = 512)
+// and by the step workgroups' helper waves (in-step, B <= 256).
+template <int LOG2B, int JM>
+__device__ __forceinline__ void la_level1(const ProcArgs &a, int jb, int c, int cur, int act, int win, int d, int l,
+                                          int f) {
+    constexpr int B = 1 << LOG2B;
     const ProcJob &J = a.job[jb];
-    const int c = a.la_all > 0 ? a.la_c0 + b : (a.la_t % LA_DM) + LA_DM * b;
-    if (c >= a.la_channels) return;
-    int cur, act, win, d;
-    if (!la_anchor_state<LOG2B>(a, jb, c, LA_DM, cur, act, win, d)) return;
-    const int tid = threadIdx.x;
-    const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
-    if (l * JM >= LA_DM) return;  // (more lanesets than window steps)
-    const int j0 = la_mid_j0(l, JM);
+    const int hi = la_hi(1, act);
+    if (hi <= LA_D0 + 1) return;
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
     const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
+    const int j0 = la_mid_j0(l, JM);
     LaAcc acc[JM];
 #pragma unroll
     for (int j = 0; j < JM; ++j) acc[j].zero();
-    la_walk<LOG2B, false, false, JM, LA_UM>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, j0, cur, act);
+    la_walk<LOG2B, false, false, JM, LA_UM>(acc, hs, xs, f * 16, f == 0, LA_D0 + 1, hi, j0, cur, act);
 #pragma unroll
     for (int j = 0; j < JM; ++j)
-        if (j0 + j >= l * JM && j0 + j < d) la_pm(a, jb, c, win, j0 + j, B)[f] = acc[j].get();
+        if (j0 + j >= l * JM && j0 + j < d) la_win(a, jb, c, win, 1, LA_P1 - d + j0 + j, B)[f] = acc[j].get();
+}
+
+// Level-1 anchor workgroup b (B = 512: the step workgroups have no helper
+// laneset to spare).
+template <int LOG2B>
+__device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int jb, int b) {
+    using LG = LaGeo<LOG2B>;
+    constexpr int F = LG::F, JM = LG::JM;
+    const int c = a.la_all > 0 ? a.la_c0 + b : (a.la_t % LA_P1) + LA_P1 * b;
+    if (c >= a.la_channels) return;
+    int cur, act, win, d;
+    if (!la_anchor_state<LOG2B>(a, jb, c, 1, cur, act, win, d)) return;
+    const int tid = threadIdx.x;
+    const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
+    if (l * JM >= LA_P1) return;  // (more lanesets than window steps)
+    la_level1<LOG2B, JM>(a, jb, c, cur, act, win, d, l, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -467,8 +407,8 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int jb, int b) 
 // process :215-295 for the common call).  Wave k < NCH runs channel k's
 // transform chain (R2C of the block into FDL row `current`, then conv, C2R,
 // overlap-add) while the other waves form every channel's
-// pre = near + (mid + far), the mid / far partials from their windows or --
-// when a level has no live window (entry, after update / reset / partial
+// pre = near + (W1 + (W2 + W3)), each level's partial from its window or --
+// when the level has no live window (entry, after update / reset / partial
 // calls) -- from chains all four waves sum first.  Two channels per
 // workgroup at B <= 256: the step and anchor workgroups of a launch then fit
 // the CUs together, so the anchors' stream runs under the transform chains.
@@ -479,8 +419,9 @@ struct LaStep {
     // channels per step workgroup (XF 3: A's and B's instance of one channel)
     static constexpr int NCH = (XF == 3 || LOG2B <= 8) ? 2 : 1;
     // B <= 256: the step workgroup's helper waves (>= one laneset of F lanes
-    // after the pre) also run the mid anchors of its channels, after the
-    // pre, under the transform chains; B = 512 launches mid anchor workgroups
+    // after the pre) also run the level-1 anchors of its channels, after the
+    // pre, under the transform chains; B = 512 launches level-1 anchor
+    // workgroups
     static constexpr bool MIDIN = LOG2B <= 8;
     // tw (the 3N/4 = 1.5B float2 the transforms index) | per channel:
     // bufA | bufB | pre (float2) | tail0 | tail1 (float) -- H[0] and the
@@ -490,13 +431,12 @@ struct LaStep {
     static constexpr size_t ch_bytes = 3 * 8 * (size_t)B + 2 * 4 * (size_t)B;
     static constexpr size_t chain_bytes = tw_bytes + NCH * ch_bytes;
     // the full pass's chain results alias the chain buffers (they are
-    // consumed before the chains start): per channel the mid chain and the NG
-    // far groups -- or, where one laneset runs every chain of a channel in
-    // order (LPW == 1), the mid chain and the WF far parts, each folded group
-    // by group as the anchors combine them
-    static constexpr int NG = la_ng<LOG2B>(), WF = LaGeo<LOG2B>::WF;
+    // consumed before the chains start): per channel the level-1 chain and
+    // the NG groups of levels 2 and 3 -- or, where one laneset runs every
+    // chain of a channel in order (LPW == 1), one slot per level, folded
+    // group by group as the anchors combine them
     static constexpr bool FOLD = LPW == 1;
-    static constexpr int GSLOTS = 1 + (FOLD ? WF : NG);
+    static constexpr int GSLOTS = FOLD ? 3 : 1 + 2 * LA_NG;
     static constexpr size_t grp_bytes = (size_t)NCH * GSLOTS * F * 16;
     // (+ the XF 3 mix counter after the chain buffers; it may alias the
     // full pass's results, which are consumed before the counter is set)
@@ -506,10 +446,10 @@ struct LaStep {
 
 // A register value the compiler must treat as produced here.  The pre's
 // "full-pass result (registers) or window row (HBM)" would otherwise be folded
-// into ONE load through a selected pointer, which moves Mreg / Freg to scratch:
-// a 32 B/lane scratch zero-fill in every step workgroup of every launch (4 MB
-// of writes per cfg2 launch, left dirty at the kernel boundary) and flat loads
-// for every window row.
+// into ONE load through a selected pointer, which moves the full-pass
+// registers to scratch: a scratch zero-fill in every step workgroup of every
+// launch (4 MB of writes per cfg2 launch in round 2, left dirty at the kernel
+// boundary) and flat loads for every window row.
 __device__ __forceinline__ float4 la_opaque(float4 v) {
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
     return v;
@@ -545,12 +485,11 @@ template <int LOG2B, bool NTL, int NCH, int XF>
 __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, const int (&cs)[NCH],
                                         const int4 (&st)[NCH], int nvalid, unsigned char *smem) {
     using LS = LaStep<LOG2B, XF>;
-    using LG = LaGeo<LOG2B>;
-    constexpr int B = LS::B, F = LS::F, LPW = LS::LPW, GPW = LG::GPW, WF = LG::WF;
+    constexpr int B = LS::B, F = LS::F, LPW = LS::LPW, NG = LA_NG;
     constexpr int HL = LA_NT - 64 * NCH;
     constexpr int TPL = (NCH * F + HL - 1) / HL;
-    constexpr int NCHAIN = 1 + LS::NG;  // full pass: mid chain + far groups, per channel
-    constexpr int GS = LS::GSLOTS;      // LDS result slots per channel (LS::FOLD: parts)
+    constexpr int NCHAIN = 1 + 2 * NG;  // full pass: level-1 chain + the groups of levels 2 and 3, per channel
+    constexpr int GS = LS::GSLOTS;      // LDS result slots per channel (LS::FOLD: one per level)
     constexpr int ROWB = B * (int)sizeof(float2);
     constexpr float invN = 1.0f / (float)(2 * B);
     constexpr size_t chb = LS::ch_bytes;
@@ -558,6 +497,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     float2 *twl = reinterpret_cast<float2 *>(smem);
     auto chan_lds = [&](int k) { return smem + LS::tw_bytes + (size_t)k * chb; };
     float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][GS][F], full pass only
+    const int nlv = a.la_nlv;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -580,19 +520,18 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     float ovr[B / 64];
     int *xcnt = reinterpret_cast<int *>(smem + LS::cnt_off);
     // the helpers leave the next block's near sum (FLAG_NEAR) where the
-    // step's pre is the launch's critical path: B = 512 (no in-step mid
+    // step's pre is the launch's critical path: B = 512 (no in-step level-1
     // anchors; the crossfade's A + B pair: helper pre 13.9 -> 9.7 us, cfg5
-    // 47.8 -> 45.8 us per step, r2j).  With in-step mid anchors (B <= 256)
-    // the far walks bound the launch and the extra helper work after the
-    // barrier lengthens the mid-anchor workgroups (cfg2 18.97 -> 19.57 us,
-    // r2j; skipping the mid-anchor channels slows their next pre instead,
-    // r2k), so those steps sum their near rows themselves.
+    // 47.8 -> 45.8 us per step, r2j).  With in-step anchors (B <= 256) the
+    // extra helper work after the barrier lengthens the anchor workgroups
+    // (cfg2 18.97 -> 19.57 us, r2j), so those steps sum their near rows
+    // themselves.
     auto near_next = [&](int) { return !LS::MIDIN; };
-    auto fullF = [&](int k) { return !la_far_live(ST(k).w); };
-    auto fullM = [&](int k) { return !la_mid_live(ST(k).w); };
+    // a level without a live window is summed by the full pass
+    auto full = [&](int k, int lv) { return lv <= nlv && !la_live(ST(k).w, lv); };
     bool anyfull = false;
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) anyfull |= k < nvalid && (fullF(k) || fullM(k));
+    for (int k = 0; k < NCH; ++k) anyfull |= k < nvalid && (full(k, 1) || full(k, 2) || full(k, 3));
 
     // helper slot t of this lane: channel k, slot f (valid if k < nvalid)
     auto task = [&](int t, int &k, int &f) {
@@ -601,9 +540,11 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         f = idx - k * F;
         return idx < NCH * F && k < nvalid;
     };
-    float4 Mreg[TPL], Freg[TPL];
+    // the full pass's level sums: level 1, and the full ones of levels 2 / 3
+    // (both: W2 + W3; one: that level's sum) -- two register sets, not three
+    float4 W1reg[TPL], W23reg[TPL];
 #pragma unroll
-    for (int t = 0; t < TPL; ++t) Mreg[t] = Freg[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = 0; t < TPL; ++t) W1reg[t] = W23reg[t] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (anyfull) {
         // the chains of the levels without a live window, into LDS
         const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
@@ -611,55 +552,56 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         for (int k = 0; k < NCH; ++k) {
             if (k >= nvalid) continue;
             const int cur = __builtin_amdgcn_readfirstlane(ST(k).x), act = __builtin_amdgcn_readfirstlane(ST(k).y);
-            const bool fm = fullM(k), ff = fullF(k);
             const RowStream hs(JK(k).H + (size_t)CS(k) * rows, bytes), xs(JK(k).X + (size_t)CS(k) * rows, bytes);
             for (int q = l; q < NCHAIN; q += LPW) {
-                if (q == 0 ? !fm : !ff) continue;
+                const int lv = q == 0 ? 1 : (q <= NG ? 2 : 3);
+                const int g = q == 0 ? 0 : (q - 1) % NG;
+                if (!full(k, lv)) continue;
                 int lo, hi;
                 if (q == 0) {
-                    lo = LA_D1 + 1;
-                    hi = LA_DF + 1;
+                    lo = LA_D0 + 1;
+                    hi = la_hi(1, act);
                 } else {
-                    la_group<LOG2B>(q - 1, act, lo, hi);
+                    la_group(lv, g, act, lo, hi);
                 }
                 LaAcc acc;
                 acc.zero();
-                if (q > 0 && la_asc(q - 1)) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
-                else la_chain<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+                if (hi > lo) {
+                    if (q > 0 && la_asc(g)) la_chain<LOG2B, true, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+                    else la_chain<LOG2B, false, NTL>(acc, hs, xs, f * 16, f == 0, lo, hi, cur, act);
+                }
                 if constexpr (LS::FOLD) {
-                    // this thread ran the earlier groups of the part: fold in
-                    // the anchors' order (group 0 of a part, then + each next)
-                    const int w = q == 0 ? -1 : (q - 1) / GPW, qq = (q - 1) % GPW;
-                    float4 *slot = &grp[(k * GS + 1 + w) * F + f];
-                    *slot = (q == 0 || qq == 0) ? acc.get() : vadd(*slot, acc.get());
+                    // this thread ran the level's earlier groups: fold in the
+                    // anchors' order (group 0, then + each next)
+                    float4 *slot = &grp[(k * GS + lv - 1) * F + f];
+                    *slot = g == 0 ? acc.get() : vadd(*slot, acc.get());
                 } else {
                     grp[(k * GS + q) * F + f] = acc.get();
                 }
             }
         }
         __syncthreads();
-        if (wave >= NCH) {  // each helper slot's mid chain and far tree (the anchors' order)
+        if (wave >= NCH) {  // each helper slot's level sums (the anchors' group order)
 #pragma unroll
             for (int t = 0; t < TPL; ++t) {
                 int k, f;
                 if (!task(t, k, f)) continue;
-                if (fullM(k)) Mreg[t] = grp[(k * GS) * F + f];
-                if (fullF(k)) {
-                    float4 A;
+                auto level = [&](int lv) {
+                    if constexpr (LS::FOLD) {
+                        return grp[(k * GS + lv - 1) * F + f];
+                    } else {
+                        if (lv == 1) return grp[(k * GS) * F + f];
+                        const int q0 = 1 + (lv - 2) * NG;
+                        float4 p = grp[(k * GS + q0) * F + f];
 #pragma unroll
-                    for (int w = 0; w < WF; ++w) {
-                        float4 pw;
-                        if constexpr (LS::FOLD) {
-                            pw = grp[(k * GS + 1 + w) * F + f];
-                        } else {
-                            pw = grp[(k * GS + 1 + w * GPW) * F + f];
-#pragma unroll
-                            for (int qq = 1; qq < GPW; ++qq) pw = vadd(pw, grp[(k * GS + 1 + w * GPW + qq) * F + f]);
-                        }
-                        A = w == 0 ? pw : vadd(A, pw);
+                        for (int g = 1; g < NG; ++g) p = vadd(p, grp[(k * GS + q0 + g) * F + f]);
+                        return p;
                     }
-                    Freg[t] = A;
-                }
+                };
+                if (full(k, 1)) W1reg[t] = level(1);
+                if (full(k, 2) && full(k, 3)) W23reg[t] = vadd(level(2), level(3));
+                else if (full(k, 2)) W23reg[t] = level(2);
+                else if (full(k, 3)) W23reg[t] = level(3);
             }
         }
         __syncthreads();  // the chain buffers below overwrite the chain results
@@ -719,7 +661,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         la_stamp(a, 1);
     } else {
         if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
-        // ---- pre = near chain (rows D1..1) + (mid + far), canonical order
+        // ---- pre = near chain (rows D0..1) + (W1 + (W2 + W3)), canonical order
 #pragma unroll
         for (int t = 0; t < TPL; ++t) {
             int k, f;
@@ -728,41 +670,38 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             const int cur = ST(k).x, act = ST(k).y, flags = ST(k).w;
             const bool nearp = (flags & FLAG_NEAR) != 0;  // the previous step left this block's near sum
             const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
-            float4 hv[LA_D1], xv[LA_D1], N0;
+            float4 hv[LA_D0], xv[LA_D0], N0;
             if (nearp) {
                 N0 = reinterpret_cast<const float4 *>(JK(k).pre + c * B)[f];
             } else {
 #pragma unroll
-                for (int i = LA_D1; i >= 1; --i) {
+                for (int i = LA_D0; i >= 1; --i) {
                     int r = cur + i;
                     if (r >= act) r -= act;
                     hv[i - 1] = hs.ld4<false>(f * 16, i * ROWB);
                     xv[i - 1] = xs.ld4<false>(f * 16, r * ROWB);
                 }
             }
-            float4 M, A;
-            if (fullM(k)) {
-                M = la_opaque(Mreg[t]);
-            } else {
-                M = la_pm(a, JB(k), c, (flags & FLAG_PWINM) ? 1 : 0, la_jm(flags), B)[f];
-            }
-            if (fullF(k)) {
-                A = la_opaque(Freg[t]);
-            } else {
-                const float4 *P0 = la_pf(a, JB(k), c, (flags & FLAG_PWIN) ? 1 : 0, la_jf(flags), 0, B);
-                A = P0[f];
-#pragma unroll
-                for (int w = 1; w < WF; ++w) A = vadd(A, P0[(size_t)w * F + f]);
-            }
+            auto wrow = [&](int lv) {
+                return la_win(a, JB(k), c, (flags & la_flag_win(lv)) ? 1 : 0, lv, la_pos((int)c, a, la_per(lv)), B)[f];
+            };
+            const float4 W1 = full(k, 1) ? la_opaque(W1reg[t]) : wrow(1);
+            const bool f2 = full(k, 2), f3 = full(k, 3);
+            float4 W23;
+            if (nlv < 3) W23 = f2 ? la_opaque(W23reg[t]) : wrow(2);
+            else if (f2 && f3) W23 = la_opaque(W23reg[t]);
+            else if (f2) W23 = vadd(la_opaque(W23reg[t]), wrow(3));
+            else if (f3) W23 = vadd(wrow(2), la_opaque(W23reg[t]));
+            else W23 = vadd(wrow(2), wrow(3));
             if (!nearp) {
                 LaAcc acc;
                 acc.zero();
 #pragma unroll
-                for (int i = LA_D1; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
+                for (int i = LA_D0; i >= 1; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 1]);
                 N0 = acc.get();
             }
             float2 *prel = reinterpret_cast<float2 *>(chan_lds(k)) + 2 * B;
-            reinterpret_cast<float4 *>(prel)[f] = vadd(N0, vadd(M, A));
+            reinterpret_cast<float4 *>(prel)[f] = vadd(N0, vadd(W1, W23));
             if constexpr (TPL > 2) __builtin_amdgcn_sched_barrier(0);  // (one task's rows in flight at a time)
         }
         la_stamp(a, 0);
@@ -785,11 +724,11 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 la_xf_arrive(a, xcnt, yA, yB, vtab, (size_t)CS(0));
             }
         }
-        // the NEXT block's near sum, rows D1..1 in the canonical order, while
-        // the chains run their C2R: rows D1..2 meet the blocks this step's
+        // the NEXT block's near sum, rows D0..1 in the canonical order, while
+        // the chains run their C2R: rows D0..2 meet the blocks this step's
         // near rows met one age earlier, row 1 meets this step's block (the
         // chain's spectrum Q, kept in LDS) -- stored in pre[] (FLAG_NEAR)
-        {
+        if constexpr (!LS::MIDIN) {
             constexpr int QOFF = fft_r2c_q_is_buf1<LOG2B>() ? B : 0;  // (the chain's Q: wave_r2c_post)
 #pragma unroll
             for (int t = 0; t < TPL; ++t) {
@@ -798,9 +737,9 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 const size_t c = (size_t)CS(k);
                 const int cur = ST(k).x, act = ST(k).y;
                 const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
-                float4 hv[LA_D1], xv[LA_D1 - 1];
+                float4 hv[LA_D0], xv[LA_D0 - 1];
 #pragma unroll
-                for (int i = LA_D1; i >= 1; --i) {
+                for (int i = LA_D0; i >= 1; --i) {
                     hv[i - 1] = hs.ld4<false>(f * 16, i * ROWB);
                     if (i >= 2) {
                         int r = cur + i - 1;
@@ -812,43 +751,32 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 LaAcc acc;
                 acc.zero();
 #pragma unroll
-                for (int i = LA_D1; i >= 2; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 2]);
+                for (int i = LA_D0; i >= 2; --i) acc.mac(la_ops(hv[i - 1], f == 0), xv[i - 2]);
                 acc.mac(la_ops(hv[0], f == 0), xq);
                 reinterpret_cast<float4 *>(JK(k).pre + c * B)[f] = acc.get();
                 if constexpr (TPL > 2) __builtin_amdgcn_sched_barrier(0);
             }
         }
-        if (a.la_probe >= 5) return;  // (timing probes 5/6: steps without their mid anchors)
         if constexpr (LS::MIDIN) {
-          if (a.la_nmid == 0) {  // (FFTCONV_LA_MIDWG: mid anchors in workgroups of their own)
-            // mid anchors of this workgroup's scheduled channels: rows DF..D1+1
-            // for the next DM steps (the pre-launch ring position is at hand)
-            constexpr int LH = HL / F;                    // helper lanesets
+            // level-1 anchors of this workgroup's scheduled channels: rows
+            // R1..D0+1 for the next P1 steps (the pre-launch ring position is
+            // at hand)
+            constexpr int LH = HL / F;  // helper lanesets
             constexpr int JMS = la_mid_per(LH);
             const int hl = tid - 64 * NCH;
             const int l = __builtin_amdgcn_readfirstlane(hl / F), f = hl % F;
-            if (l * JMS < LA_DM) {
+            if (l * JMS < LA_P1) {
 #pragma unroll
                 for (int k = 0; k < NCH; ++k) {
-                    if (k >= nvalid || !la_sched(CS(k), a, LA_DM)) continue;
-                    const size_t c = (size_t)CS(k);
+                    if (k >= nvalid || !la_sched(CS(k), a, LA_P1)) continue;
+                    const int c = CS(k);
                     const int cur = __builtin_amdgcn_readfirstlane(ST(k).x);
                     const int act = __builtin_amdgcn_readfirstlane(ST(k).y);
                     const int flags = __builtin_amdgcn_readfirstlane(ST(k).w);
-                    const int win = (flags & FLAG_PWINM) ? 0 : 1, d = la_dnew((int)c, a, LA_DM);
-                    const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
-                    LaAcc acc[JMS];
-#pragma unroll
-                    for (int j = 0; j < JMS; ++j) acc[j].zero();
-                    const int j0 = la_mid_j0(l, JMS);
-                    la_walk<LOG2B, false, false, JMS, LA_UM>(acc, hs, xs, f * 16, f == 0, LA_D1 + 1, LA_DF + 1, j0, cur,
-                                                         act);
-#pragma unroll
-                    for (int j = 0; j < JMS; ++j)
-                        if (j0 + j >= l * JMS && j0 + j < d) la_pm(a, JB(k), c, win, j0 + j, B)[f] = acc[j].get();
+                    const int win = (flags & FLAG_PW1) ? 0 : 1, d = la_dnew(c, a, LA_P1);
+                    la_level1<LOG2B, JMS>(a, JB(k), c, cur, act, win, d, l, f);
                 }
             }
-          }
         }
         return;
     }
@@ -900,16 +828,11 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         if (lane == 0) {
             const int curp = cur > 0 ? cur - 1 : act - 1;  // :287-291
             int nf = (keep ^ FLAG_REV) | tag | (near_next(k) ? FLAG_NEAR : 0);  // (the helpers stored it)
-            // far window: open (a far anchor this launch), advance, or drop
-            if (la_sched((int)c, a, LA_DF))
-                nf = (nf ^ FLAG_PWIN) | FLAG_LA | ((la_dnew((int)c, a, LA_DF) - 1) << LA_D_SHIFT);
-            else if (la_far_live(flags))
-                nf |= FLAG_LA | ((la_jf(flags) + 1) << LA_J_SHIFT) | ((la_df(flags) - 1) << LA_D_SHIFT);
-            // mid window
-            if (la_sched((int)c, a, LA_DM))
-                nf = (nf ^ FLAG_PWINM) | FLAG_LAM | ((la_dnew((int)c, a, LA_DM) - 1) << LA_DM_SHIFT);
-            else if (la_mid_live(flags))
-                nf |= FLAG_LAM | ((la_jm(flags) + 1) << LA_JM_SHIFT) | ((la_dm(flags) - 1) << LA_DM_SHIFT);
+            // per level: open a window (an anchor this launch), keep it, or drop it
+            for (int lv = 1; lv <= nlv; ++lv) {
+                if (la_sched((int)c, a, la_per(lv))) nf = (nf ^ la_flag_win(lv)) | la_flag_live(lv);
+                else if (la_live(flags, lv)) nf |= la_flag_live(lv);
+            }
             JC.state[c] = make_int4(curp, act, 0, nf);
         }
     } else {
@@ -1001,8 +924,6 @@ __device__ __attribute__((noinline)) void la_fallback_xf(const ProcArgs *ap, int
     for (int j = threadIdx.x; j < m.n; j += LA_NT) o[j] = mix_select(ya[j], yb[j], mix_selector(m, j, t));
 }
 
-// grid: [far anchors | mid anchors | step workgroups] (or the steps first);
-// XF 3: [A's far | B's far | A's mid | B's mid | one workgroup per channel]
 constexpr int LA_XWG = 8;  // A's launch: leading workgroups (the first writes the mix_value walk)
 
 // crossfade, A's launch: per-sample mix selectors of this call for B's
@@ -1031,26 +952,35 @@ __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsign
     for (int j = threadIdx.x; j < m.n; j += LA_NT) mt[j] = mix_selector(m, j, t);
 }
 
-// XF 3 grid order (ProcArgs::la_steps_first) -> the block's index in the
-// logical order [far A | far B | mid A | mid B | steps], or -1 (padding):
-//   0: logical order; 1: the channels' step workgroups lead the grid (the
-//   latency-critical chains get the CUs first, the anchors fill in);
-//   2: steps, then the mid anchors (padded to a multiple of 8 blocks), then the
-//   far anchors -- the mid anchors start with the launch instead of waiting
-//   for the far walks' slots.  The far anchors keep their XCD placement when
-//   the channel count is a multiple of 8 (nf is one).
-__device__ __forceinline__ int la_xf3_block(const ProcArgs &a) {
-    const int nf = a.la_nfar, nm = a.la_nmid;
-    int b = (int)blockIdx.x;
-    if (a.la_steps_first == 0) return b;
-    if (b < a.la_channels) return b + 2 * (nf + nm);
-    b -= a.la_channels;
-    if (a.la_steps_first == 1) return b;
-    const int mp = (2 * nm + 7) / 8 * 8;
-    if (b < mp) return b < 2 * nm ? 2 * nf + b : -1;
-    return b - mp;
+// Anchor workgroup ba of the grid's anchor block [level 3 | level 2 | level 1]
+// (la_n[2], la_n[1], la_n[0] workgroups) of instance jb; false if ba is past it.
+// The level-3 and level-2 counts are whole XCD rounds (multiples of 8), so
+// every anchor keeps its XCD placement.
+template <int LOG2B, bool NTL>
+__device__ __forceinline__ bool la_anchor(const ProcArgs &a, int jb, int ba, unsigned char *smem) {
+    if (ba < a.la_n[2]) {
+        la_anchor_far<LOG2B, 3, NTL>(a, jb, ba, smem);
+        return true;
+    }
+    ba -= a.la_n[2];
+    if (ba < a.la_n[1]) {
+        la_anchor_far<LOG2B, 2, NTL>(a, jb, ba, smem);
+        return true;
+    }
+    ba -= a.la_n[1];
+    if (ba < a.la_n[0]) {
+        la_anchor_mid<LOG2B>(a, jb, ba);
+        return true;
+    }
+    return false;
 }
 
+// grid (XF 0 / 1 / 2): [the 8 mix-walk workgroups (XF 1) | level 3 | level 2 |
+// level 1 anchors | step workgroups].  XF 3: [one step workgroup per channel |
+// A's level 3 | B's level 3 | A's level 2 | B's level 2 | A's level 1 | B's
+// level 1] -- the latency-critical chains get the CUs first, the anchors fill
+// in (each level's count is a multiple of 8: B's anchors keep their XCD
+// placement).
 // XF: crossfade role of the launch (ProcArgs::la_mix): 0 none; 1 = A's launch,
 // whose first workgroup also writes the gains of this call's mix_value walk to mix_tab;
 // 2 = B's launch, whose steps mix A's block with their own
@@ -1059,24 +989,23 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
     using LS = LaStep<LOG2B, XF>;
     constexpr int NCH = LS::NCH;
     if constexpr (XF == 3) {
-        const int nf = a.la_nfar, nm = a.la_nmid;
-        const int b = la_xf3_block(a);
-        if (b < 0) return;
-        // (timing / traffic probes, results wrong: 1 steps only, 2 anchors
-        // only, 3 far anchors only, 4 mid anchors only)
-        const int pr = a.la_probe;
-        if (b < 2 * nf) {  // (nf is a multiple of 8: B's far anchors keep the XCD placement)
-            if (pr != 1 && pr != 4) la_anchor_far<LOG2B, NTL>(a, b >= nf ? 1 : 0, b >= nf ? b - nf : b, smem);
+        int b = (int)blockIdx.x;
+        if (b >= a.la_channels) {
+            b -= a.la_channels;
+            for (int lv = 3; lv >= 1; --lv) {
+                const int n = a.la_n[lv - 1];
+                if (b < 2 * n) {
+                    const int jb = b >= n ? 1 : 0, ba = b - jb * n;
+                    if (lv == 3) la_anchor_far<LOG2B, 3, NTL>(a, jb, ba, smem);
+                    else if (lv == 2) la_anchor_far<LOG2B, 2, NTL>(a, jb, ba, smem);
+                    else la_anchor_mid<LOG2B>(a, jb, ba);
+                    return;
+                }
+                b -= 2 * n;
+            }
             return;
         }
-        if (b < 2 * (nf + nm)) {
-            const int bm = b - 2 * nf;
-            if (pr != 1 && pr != 3) la_anchor_mid<LOG2B, NTL>(a, bm >= nm ? 1 : 0, bm >= nm ? bm - nm : bm);
-            return;
-        }
-        if (pr >= 2 && pr <= 4) return;
-        const int c = b - 2 * (nf + nm);
-        if (c >= a.la_channels) return;
+        const int c = b;
         const int4 va = a.job[0].state[c], vb = a.job[1].state[c];
         const int4 st[2] = {make_int4(__builtin_amdgcn_readfirstlane(va.x), __builtin_amdgcn_readfirstlane(va.y),
                                       __builtin_amdgcn_readfirstlane(va.z), __builtin_amdgcn_readfirstlane(va.w)),
@@ -1090,7 +1019,7 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
         return;
     }
     if constexpr (XF == 1) {
-        // 8 extra workgroups at the front of the grid (one per XCD: the far
+        // 8 extra workgroups at the front of the grid (one per XCD: the
         // anchors' XCD placement behind them is unchanged); the first walks,
         // so the walk starts with the launch and runs beside the steps
         if (blockIdx.x < LA_XWG) {
@@ -1098,22 +1027,13 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
             return;
         }
     }
-    const int nanchor = a.la_nfar + a.la_nmid;
-    const int nstep = (int)gridDim.x - nanchor - (XF == 1 ? LA_XWG : 0);  // step workgroups
+    const int nanchor = a.la_n[0] + a.la_n[1] + a.la_n[2];
     const int b = (int)blockIdx.x - (XF == 1 ? LA_XWG : 0);
-    const int ba = a.la_steps_first ? b - nstep : b;  // anchor index, < 0 for a step
-    if (ba >= 0 && ba < nanchor) {
-        if (a.la_probe != 1 && a.la_probe != 6) {
-            if (ba < a.la_nfar) {
-                if (a.la_probe != 4) la_anchor_far<LOG2B, NTL>(a, 0, ba, smem);
-            } else if (a.la_probe != 3) {
-                la_anchor_mid<LOG2B, NTL>(a, 0, ba - a.la_nfar);
-            }
-        }
+    if (b < nanchor) {
+        la_anchor<LOG2B, NTL>(a, 0, b, smem);
         return;
     }
-    if (a.la_probe >= 2 && a.la_probe <= 4) return;
-    const int c0 = (a.la_steps_first ? b : b - nanchor) * NCH;
+    const int c0 = (b - nanchor) * NCH;
     const ProcJob &J = a.job[0];
     const int nvalid = min(NCH, a.la_channels - c0);
     int cs[NCH];
@@ -1134,20 +1054,29 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
         la_fallback<LOG2B, NTL, XF>((const ProcArgs *)__builtin_amdgcn_kernarg_segment_ptr(), c0, nvalid, smem);
 }
 
-// the role of workgroup blockIdx.x in a lookahead launch (for the timeline)
+// the role of workgroup blockIdx.x in a lookahead launch (for the timeline):
+// 0 level-3 anchor, 1 level-2 anchor, 2 step, 3 level-1 anchor, 4 mix walk, 5 padding
 template <int XF>
 __device__ __forceinline__ int la_role(const ProcArgs &a) {
+    int b = (int)blockIdx.x;
     if (XF == 3) {
-        const int b = la_xf3_block(a);
-        return b < 0 ? 5 : b < 2 * a.la_nfar ? 0 : (b < 2 * (a.la_nfar + a.la_nmid) ? 1 : 2);
+        if (b < a.la_channels) return 2;
+        b -= a.la_channels;
+        if (b < 2 * a.la_n[2]) return 0;
+        b -= 2 * a.la_n[2];
+        if (b < 2 * a.la_n[1]) return 1;
+        b -= 2 * a.la_n[1];
+        return b < 2 * a.la_n[0] ? 3 : 5;
     }
-    if (XF == 1 && blockIdx.x < LA_XWG) return 4;  // mix walk
-    const int nanchor = a.la_nfar + a.la_nmid;
-    const int nstep = (int)gridDim.x - nanchor - (XF == 1 ? LA_XWG : 0);
-    const int b = (int)blockIdx.x - (XF == 1 ? LA_XWG : 0);
-    const int ba = a.la_steps_first ? b - nstep : b;
-    if (ba >= 0 && ba < nanchor) return ba < a.la_nfar ? 0 : 1;  // far / mid anchor
-    return 2;                                                       // step
+    if (XF == 1) {
+        if (b < LA_XWG) return 4;
+        b -= LA_XWG;
+    }
+    if (b < a.la_n[2]) return 0;
+    b -= a.la_n[2];
+    if (b < a.la_n[1]) return 1;
+    b -= a.la_n[1];
+    return b < a.la_n[0] ? 3 : 2;
 }
 
 template <int LOG2B, bool NTL, int XF>

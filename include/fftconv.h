@@ -95,15 +95,19 @@ int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *inp
  * the stand-alone mix kernel (by default B's launch mixes in its epilogue,
  * from gains A's launch precomputed; bit-identical either way), bit 7 = IR
  * transforms (init / update) one segment per workgroup (by default one per
- * wave for 64 <= B <= 1024; bit-identical).
+ * wave for 64 <= B <= 1024; bit-identical), bit 8 = two-stage tail0 runs
+ * per head block (by default its blocks are convolved together at the end
+ * of each tail period; read when a TwoStageFFTConvolver is created).
  * Lookahead (automatic for standalone FFTConvolver batches with
  * 128 <= B <= 512 and >= 40 segments, full-block calls from an empty input
- * buffer): the FDL sum of each block is re-associated in time over three
- * levels -- the step sums rows 1..5 itself, a mid anchor every 5 blocks sums
- * rows 6..32 for the next 5 blocks, a far anchor every 32 blocks sums rows
- * >= 33 for the next 32 blocks -- so a full-block call streams ~1/9 of the
- * reference's bytes; its summation order does not depend on the channel
- * index, the shard or the call history (bit-identical to summing every row).
+ * buffer): the FDL sum of each block is re-associated in time over a near
+ * level and three anchor levels with geometric periods -- the step sums
+ * rows 1..4 itself, an anchor every 4 blocks sums rows 5..16 for the next 4
+ * blocks, one every 16 blocks rows 17..64 for the next 16, one every 64
+ * blocks rows >= 65 for the next 64 -- so a full-block call streams ~1/10
+ * of the reference's bytes; its summation order does not depend on the
+ * channel index, the shard or the call history (bit-identical to summing
+ * every row).
  * -1 selects automatic; any other negative value is FFTCONV_E_INVALID.
  * Results agree within f32 rounding across variants. */
 int fftconv_set_kernel_variant(int variant);

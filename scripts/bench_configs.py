@@ -189,7 +189,7 @@ def main():
         T = conv.tail_block_size
         samples = C * head * a.steps3
         canon_sample = (uniform_bytes(head, T) + uniform_bytes(head, T) + uniform_bytes(T, L - 2 * T) * head / T) / head
-        defer = os.environ.get("FFTCONV_TAIL0_DEFER", "1") != "0"  # (host.cpp TwoStageCore::t0_defer)
+        defer = a.variant < 0 or not (a.variant & 256)  # (VARIANT_T0BLOCK, host.cpp TwoStageCore::t0_defer)
         tail0_b = tail0_deferred_bytes_per_block(head, T) if defer else uniform_bytes(head, T)
         per_sample = (uniform_bytes(head, T) + tail0_b + uniform_bytes(T, L - 2 * T) * head / T) / head
         if a.sweep:
@@ -240,8 +240,7 @@ def main():
         samples = C * B * a.steps5
         # both inner convolvers on the lookahead step unless variant bit 4 is set
         la = a.variant < 0 or not (a.variant & 16)
-        parts = 1  # far window parts (LaGeo::WF: 4 far groups, one bin slice per 4-wave workgroup)
-        per_sample = 2 * (lookahead_bytes_per_channel_block(B, L, parts) if la else uniform_bytes(B, L)) / B
+        per_sample = 2 * (lookahead_bytes_per_channel_block(B, L) if la else uniform_bytes(B, L)) / B
         out.append({"config": "cfg5 CrossfadeConvolver, update every 128 blocks", "channels": C, "block": B,
                     "ir": L, "steps": a.steps5, "MSamples_s": round(samples / t / 1e6, 2),
                     "us_per_step": round(t / a.steps5 * 1e6, 3),

@@ -1,9 +1,9 @@
 """The lookahead step (fft-convolution_amd/csrc/la.hpp) on the device.
 
 FFTConvolver::process (src/fft_convolver.rs:215-295) for a full block with
-the FDL sum re-associated in time: the step sums rows 1..5, mid anchors sum
-rows 6..32 five blocks ahead, far anchors rows >= 33 thirty-two blocks ahead
-(S >= 40).  Checked against the oracle (tolerance REL_TOL, as every
+the FDL sum re-associated in time: the step sums rows 1..4, anchors sum rows
+5..16 four blocks ahead, rows 17..64 sixteen blocks ahead and rows >= 65
+sixty-four blocks ahead (S >= 40; the third anchor level exists when S > 65).  Checked against the oracle (tolerance REL_TOL, as every
 parity test), and for the property the design rests on -- the summation
 order is canonical, so the bits do not depend on a channel's stagger phase,
 its index, the shard it sits in, or whether a step was served from a window
@@ -258,3 +258,64 @@ def test_lookahead_crossfade_fused_mix(amd, oracle_mod, B, L):
         m = ~np.isnan(exp[c])
         assert np.array_equal(np.isnan(outs[-1][c]), ~m), c
         assert_close(outs[-1][c][m], exp[c][m], what=f"fused ch {c}")
+
+
+@pytest.mark.parametrize("B", [128, 256, 512])
+def test_lookahead_three_levels_vs_oracle(amd, oracle_mod, B):
+    """An FDL long enough for the third anchor level (rows >= 65, one anchor
+    every 64 blocks): > 3 level-3 windows per channel, a partial call (the
+    windows drop and re-enter), an update that shrinks the active segments
+    below the third level's first row and one that restores them, against
+    the oracle every block."""
+    rng = np.random.default_rng(500 + B)
+    C, L = 5, 150 * B - 9
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    assert conv.lookahead_parts() > 0
+    refs = _refs(oracle_mod, hs, B, L)
+    chunks = [B] * 230 + [B // 4, B - B // 4] + [B] * 80 + [B] * 70 + [B] * 80
+    ups = {312: L - 100 * B, 382: L}  # 50 active segments, then all 150 again
+    for j, k in enumerate(chunks):
+        if j in ups:
+            hn = np.stack([ir(rng, ups[j]) for _ in range(C)])
+            conv.update(hn)
+            for c in range(C):
+                refs[c].update(hn[c])
+        x = np.stack([white(rng, k) for _ in range(C)])
+        got = conv.process(x)
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"B={B} chunk {j} ch {c}")
+    for c in range(C):
+        assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
+
+
+def test_lookahead_three_levels_phase_and_full_sum(amd):
+    """70 identical channels cover all 64 level-3 stagger phases: every
+    channel's output is bit-identical to channel 0's, and to a batch whose
+    steps sum every row themselves (VARIANT_LAFULL), through a partial call,
+    a re-entry and an update."""
+    rng = np.random.default_rng(520)
+    C, B, L = 70, 256, 140 * 256
+    h = ir(rng, L)
+    hn = ir(rng, L - 300)
+    xs = [white(rng, B) for _ in range(260)]
+    outs = {}
+    for v in (-1, LAFULL):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.FFTConvolver.init(np.tile(h, (C, 1)), B, L, channels=C)
+            ys = []
+            for j, x in enumerate(xs):
+                if j == 200:
+                    conv.update(np.tile(hn, (C, 1)))
+                if j == 150:
+                    ys.append(conv.process(np.tile(x[:100], (C, 1))))
+                    ys.append(conv.process(np.tile(x[100:], (C, 1))))
+                else:
+                    ys.append(conv.process(np.tile(x, (C, 1))))
+            outs[v] = np.concatenate(ys, axis=1)
+        finally:
+            amd.set_kernel_variant(-1)
+    for c in range(1, C):
+        assert np.array_equal(outs[-1][c], outs[-1][0]), c
+    assert np.array_equal(outs[-1], outs[LAFULL])

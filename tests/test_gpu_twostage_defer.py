@@ -105,36 +105,23 @@ def test_deferred_batch_one_channel_replays(amd, oracle_mod):
     _run(conv, ref, rng, [head] * (3 * per + 4), nan_at=[(per + 3, 2, 40)], channels=C)
 
 
-_PER_BLOCK = r"""
-import sys
-import numpy as np
-sys.path[:0] = [{pkg!r}, {orc!r}, {tst!r}]
-import fftconv_amd as F
-import oracle as O
-from common import assert_close, ir, white
-rng = np.random.default_rng(10)
-head, L = 64, 12000
-h = ir(rng, L)
-conv = F.TwoStageFFTConvolver.init(h, head, L)
-ref = O.TwoStageFFTConvolver.init(h, head, L)
-T = ref.tail_block_size
-chunks = [head] * (T // head + 5) + [13, 51] + [head] * (2 * T // head)
-got = np.concatenate([conv.process(white(np.random.default_rng(k), n)) for k, n in enumerate(chunks)])
-exp = np.concatenate([ref.process(white(np.random.default_rng(k), n)) for k, n in enumerate(chunks)])
-assert_close(got, exp, what="per-block tail0")
-print("ok")
-"""
+T0BLOCK = 256  # VARIANT_T0BLOCK (include/fftconv.h): per-block tail0, read at create
 
 
-def test_per_block_tail0_path(amd):
-    """FFTCONV_TAIL0_DEFER=0 (read once per process, so in a child): the
-    per-block tail0 launch of round 1 still matches the oracle."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = _PER_BLOCK.format(pkg=os.path.join(root, "fft-convolution_amd"), orc=os.path.join(root, "oracle"),
-                             tst=os.path.join(root, "tests"))
-    env = dict(os.environ, FFTCONV_TAIL0_DEFER="0")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+def test_per_block_tail0_path(amd, oracle_mod):
+    """Variant bit 8 (VARIANT_T0BLOCK, read when the convolver is created):
+    the per-block tail0 launch of round 1 still matches the oracle."""
+    rng = np.random.default_rng(10)
+    head, L = 64, 12000
+    h = ir(rng, L)
+    amd.set_kernel_variant(T0BLOCK)
+    try:
+        conv = amd.TwoStageFFTConvolver.init(h, head, L)
+    finally:
+        amd.set_kernel_variant(-1)
+    ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
+    T = ref.tail_block_size
+    chunks = [head] * (T // head + 5) + [13, 51] + [head] * (2 * T // head)
+    got = np.concatenate([conv.process(white(np.random.default_rng(k), n)) for k, n in enumerate(chunks)])
+    exp = np.concatenate([ref.process(white(np.random.default_rng(k), n)) for k, n in enumerate(chunks)])
+    assert_close(got, exp, what="per-block tail0")
