@@ -221,7 +221,12 @@ struct UniformCore {
     DevPtr<int4> state;
     hipStream_t stream = nullptr;
     Scratch scratch;
-    PinnedStage hstage;            // host IR uploads (update_host), [C][ir_len]
+    // host IR uploads (update_host), [C][ir_len]: only a standalone batch
+    // owns one (own_stage, set before init).  A crossfade's a / b stage
+    // through the crossfade's, and a two-stage's inner convolvers are never
+    // updated (TwoStageFFTConvolver::update is todo!(), :408-410).
+    PinnedStage hstage;
+    bool own_stage = false;
     mutable StreamOrder order;     // (clone_from drains its source)
     // lookahead (la.hpp): standalone batches only (la_ok, set before init)
     bool la_ok = false;
@@ -283,7 +288,8 @@ struct UniformCore {
         if (int r = state.alloc(C)) return r;
         if (int r = tw.alloc(2 * B)) return r;
         if (int r = staging.alloc(C * ir_len)) return r;  // update() never allocates
-        if (int r = hstage.alloc(C * ir_len)) return r;
+        if (own_stage)
+            if (int r = hstage.alloc(C * ir_len)) return r;
         la_W = la_ok ? la_parts(log2b, (int)S) : 0;
         if (la_W) {
             const LaDims d = la_dims(log2b, (int)S);
@@ -398,18 +404,22 @@ struct UniformCore {
         // and the transform are enqueued behind the handle's previous work,
         // and every later call is ordered behind them (StreamOrder)
         if (int r = order.enter(stream)) return r;
-        return update_host_on(chan0, nch, src, len, stride, stream);
+        return update_host_on(chan0, nch, src, len, stride, stream, hstage, ir_len);
     }
-    // (the caller has ordered stream s behind the handle's previous work)
-    int update_host_on(size_t chan0, size_t nch, const float *src, size_t len, size_t stride, hipStream_t s) {
+    // (the caller has ordered stream s behind the handle's previous work);
+    // the response goes through `stage`, rows of `row` >= len floats
+    int update_host_on(size_t chan0, size_t nch, const float *src, size_t len, size_t stride, hipStream_t s,
+                       PinnedStage &stage, size_t row) {
         if (len > ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
         if (ir_len == 0) return FFTCONV_OK;
-        if (int r = hstage.acquire()) return r;
         const size_t sst = (stride == 0 && nch > 1) ? 0 : ir_len;
         if (len && nch) {
-            hstage.fill(src, nch, len, stride == 0 && nch > 1 ? 0 : stride, ir_len);
-            if (int r = upload(chan0, sst ? nch : 1, hstage.p, len, ir_len, s)) return r;
-            if (int r = hstage.release(s)) return r;
+            if (len > row || stage.n < (sst ? nch : 1) * row)
+                return fail(FFTCONV_E_INVALID, "no host staging for this update");
+            if (int r = stage.acquire()) return r;
+            stage.fill(src, nch, len, stride == 0 && nch > 1 ? 0 : stride, row);
+            if (int r = upload(chan0, sst ? nch : 1, stage.p, len, row, s)) return r;
+            if (int r = stage.release(s)) return r;
         }
         return ir_from_device(chan0, nch, staging.p + chan0 * ir_len, sst, len, len, true, s);
     }
@@ -443,8 +453,9 @@ struct UniformCore {
         return j;
     }
 
-    // a full-block call takes the lookahead launch
-    bool la_ready(size_t n) const { return la_W && n == B && la_parts(log2b, (int)S) == la_W; }
+    // a call of whole blocks takes the lookahead launch, one
+    // launch per block
+    bool la_ready(size_t n) const { return la_W && n > 0 && n % B == 0 && la_parts(log2b, (int)S) == la_W; }
 
     // this batch's lookahead fields of a launch: windows, stagger clock (the
     // launcher derives the anchor workgroups from them), and the timeline
@@ -454,7 +465,7 @@ struct UniformCore {
         a.la_all = la_all ? 1 : 0;
         a.la_t = (int)(la_t % (unsigned long long)la_dims(log2b, (int)S).per_all);  // (every period divides it)
         a.la_seq = la_seq;
-        if (trace_slots) {
+        if (trace_slots && !la_all) {  // (steady-state launches only: the record is sized for them)
             const size_t slot = (size_t)(la_t % trace_slots);
             a.la_trace = trace.p + slot * trace_grid * 8;
             a.la_trace_grid = (int)trace_grid;
@@ -481,17 +492,27 @@ struct UniformCore {
         a.tw = tw.p;
         a.njobs = 1;
         if (la_ready(n)) {
-            // lookahead launch: the step workgroups behind this launch's far
-            // and mid anchors (every channel on entry, else the stagger
-            // classes (c - t) % period == 0)
-            if (int r = la_fill(a, s)) return r;
-            if (la_mix && mix) {
-                a.la_mix = la_mix;
-                a.mix = *mix;
-                a.mix_tab = mix_tab;
+            // lookahead launches, one per block of the call: the step
+            // workgroups behind each launch's anchors (every channel on entry,
+            // else the stagger classes (c - t) % period == 0).  A multi-block
+            // call keeps the windows: each launch is the step of one block,
+            // bit-identical to one call per block; a channel off the lookahead
+            // path runs the whole call (:222-294) in the first launch
+            const size_t m = n / B;
+            if (m > 1 && la_mix) return fail(FFTCONV_E_INVALID, "crossfade lookahead launch of more than one block");
+            for (size_t k = 0; k < m; ++k) {
+                a.job[0] = job(din + k * B, is, dout + k * B, os, B);
+                a.job[0].mcall = (int)m;
+                a.job[0].mk = (int)k;
+                if (int r = la_fill(a, s)) return r;
+                if (la_mix && mix) {
+                    a.la_mix = la_mix;
+                    a.mix = *mix;
+                    a.mix_tab = mix_tab;
+                }
+                HIP_TRY(launch_process_la(log2b, a, (int)C, s));
+                la_advance();
             }
-            HIP_TRY(launch_process_la(log2b, a, (int)C, s));
-            la_advance();
             return FFTCONV_OK;
         }
         if (la_W) la_all = true;  // this launch drops every window
@@ -514,7 +535,7 @@ struct UniformCore {
     }
 
     // #[derive(Clone)]
-    int clone_from(const UniformCore &o) {
+    int clone_from(const UniformCore &o, bool with_stage = true) {
         DeviceGuard g(o.device);
         if (int r = o.order.drain(o.stream)) return r;
         device = o.device;
@@ -542,7 +563,9 @@ struct UniformCore {
             trace_meta.assign(2 * trace_slots, -1);
         }
         if (int r = staging.alloc(o.staging.n)) return r;
-        if (int r = hstage.alloc(o.hstage.n)) return r;
+        own_stage = with_stage && o.own_stage;
+        if (own_stage)
+            if (int r = hstage.alloc(o.hstage.n)) return r;
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -698,8 +721,8 @@ struct TwoStageCore {
         a.xs = t0_xs.p; a.ys = t0_ys.p; a.err = t0_err.p; a.ov0 = t0_ov.p; a.cv = t0_cv.p;
         a.act = (int)tail0->S;
         a.n = (int)t0_n; a.nmax = (int)t0_nmax;
-        t0_n = 0;
         HIP_TRY(launch_tail0_flush(tail0->log2b, a, (int)C, s));
+        t0_n = 0;  // (only once the flush is enqueued: a failed launch keeps the blocks pending)
         return FFTCONV_OK;
     }
 
@@ -792,15 +815,17 @@ struct TwoStageCore {
             a.job[0].tin = tail_input() + tail_input_fill;                     // :459-461
             a.job[0].tin_stride = (long long)T;
             a.njobs = 1;
-            if (tail0 && t0_defer) {                                            // :464-472, deferred
-                if (t0_n == 0) t0_off = tail_input_fill;
-                ++t0_n;
-            } else if (tail0) {                                                 // :464-472
+            const bool defer_block = tail0 && t0_defer;                        // :464-472, deferred
+            if (tail0 && !defer_block) {                                        // :464-472
                 a.job[1] = tail0->job(din, is, tail_output0 + tail_input_fill, T, head_bs);
                 a.njobs = 2;
             }
             a.tw = head->tw.p;
             HIP_TRY(launch_process(head->log2b, a, (int)C, s));
+            if (defer_block) {  // (counted once the head launch that writes its tail_input is enqueued)
+                if (t0_n == 0) t0_off = tail_input_fill;
+                ++t0_n;
+            }
             precalculated_pos += len;
             tail_input_fill += len;
             if (tail_input_fill == T) {
@@ -962,6 +987,7 @@ struct Crossfader {
 struct CrossfadeCore {
     int device = 0;
     size_t C = 0, max_buffer_size = 0, stored_len = 0, stored_stride = 0;
+    size_t stage_row = 0;  // hstage row: the stored response, or a direct update of a / b
     std::unique_ptr<UniformCore> a, b;
     Crossfader xf;
     DevPtr<float> buf_a, buf_b, stored;
@@ -1010,8 +1036,8 @@ struct CrossfadeCore {
         a.reset(new (std::nothrow) UniformCore());
         b.reset(new (std::nothrow) UniformCore());
         if (!a || !b) return fail(FFTCONV_E_NOMEM, "out of host memory");
-        if (int r = a->clone_from(conv)) return r;
-        if (int r = b->clone_from(conv)) return r;
+        if (int r = a->clone_from(conv, false)) return r;  // (update() stages through hstage below)
+        if (int r = b->clone_from(conv, false)) return r;
         // A and B start as copies: equal FDLs (FLAG_XSYNC), and one
         // active_seg_count if every channel of `conv` has the same
         if (C) {
@@ -1028,7 +1054,8 @@ struct CrossfadeCore {
         stored_stride = stored_len;
         if (int r = stored.alloc(C * stored_len)) return r;
         if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), stream));
-        if (int r = hstage.alloc(C * stored_len)) return r;
+        stage_row = std::max(stored_len, a->ir_len);
+        if (int r = hstage.alloc(C * stage_row)) return r;
         xf.init(crossfade_samples, std::min(mbs, max_response_length));
         max_buffer_size = mbs;
         if (int r = buf_a.alloc(C * mbs)) return r;
@@ -1117,7 +1144,7 @@ struct CrossfadeCore {
         if (!is_crossfading()) {
             UniformCore &t = xf.target == 0 ? *b : *a;
             if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
-            if (int r = t.update_host_on(0, C, src, len, stride, stream)) return r;
+            if (int r = t.update_host_on(0, C, src, len, stride, stream, hstage, stage_row)) return r;
             note_update(xf.target == 0 ? 1 : 0, len);
             xf.fade_into(xf.target == 0 ? 1 : 0);
             response_pending = false;
@@ -1310,6 +1337,7 @@ struct CrossfadeCore {
         if (int r = buf_b.alloc(o.buf_b.n)) return r;
         if (int r = mix_tab.alloc(o.mix_tab.n)) return r;
         if (int r = stored.alloc(o.stored.n)) return r;
+        stage_row = o.stage_row;
         if (int r = hstage.alloc(o.hstage.n)) return r;
         if (stored.n) HIP_TRY(hipMemcpyAsync(stored.p, o.stored.p, stored.bytes(), hipMemcpyDeviceToDevice, stream));
         HIP_TRY(hipStreamSynchronize(stream));
@@ -1319,8 +1347,10 @@ struct CrossfadeCore {
 
 // W_N^k tables of the stand-alone Fft entry points, one per (device, N),
 // built on first use in f64 and kept for the process (the handles keep
-// their own); the same values as every handle's table for that N.
-int fft_twiddles(int dev, int log2n, const float2 **out) {
+// their own); the same values as every handle's table for that N.  The first
+// use uploads on the caller's stream and waits for that stream only (no
+// legacy-stream synchronisation).
+int fft_twiddles(int dev, int log2n, hipStream_t s, const float2 **out) {
     static std::mutex mu;
     static std::map<std::pair<int, int>, float2 *> tabs;
     std::lock_guard<std::mutex> lk(mu);
@@ -1337,7 +1367,12 @@ int fft_twiddles(int dev, int log2n, const float2 **out) {
     }
     float2 *p = nullptr;
     HIP_TRY(hipMalloc((void **)&p, N * sizeof(float2)));
-    HIP_TRY(hipMemcpy(p, t.data(), N * sizeof(float2), hipMemcpyHostToDevice));
+    hipError_t e = hipMemcpyAsync(p, t.data(), N * sizeof(float2), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // (t is freed on return)
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return fail(FFTCONV_E_DEVICE, std::string("twiddle upload: ") + hipGetErrorString(e));
+    }
     tabs[{dev, log2n}] = p;
     *out = p;
     return FFTCONV_OK;
@@ -1355,7 +1390,7 @@ int fft_rows(int device, size_t n, size_t rows, const float *din, size_t is, flo
     if (rows == 0) return FFTCONV_OK;
     DeviceGuard g(device);
     const float2 *tw = nullptr;
-    if (int r = fft_twiddles(device, ilog2(n), &tw)) return r;
+    if (int r = fft_twiddles(device, ilog2(n), s, &tw)) return r;
     FftArgs a{};
     a.in = din; a.in_stride = (long long)is; a.out = dout; a.out_stride = (long long)os; a.tw = tw; a.status = status;
     HIP_TRY(launch_fft_rows(ilog2(n) - 1, inverse, a, (int)rows, s));
@@ -1477,6 +1512,7 @@ fftconv_uniform *fftconv_uniform_init_batch(int device, size_t channels, const f
     auto *h = new (std::nothrow) fftconv_uniform();
     if (!h) { set_error("out of host memory"); return nullptr; }
     h->core.la_ok = true;
+    h->core.own_stage = true;
     int r = h->core.init(device, channels, responses, response_len, response_stride, max_block_size,
                          max_response_length);
     return make_or_null(r, h);

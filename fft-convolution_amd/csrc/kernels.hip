@@ -1278,12 +1278,17 @@ __global__ __launch_bounds__(NT) void fft_rows_kernel(FftArgs a) {
         constexpr float invN = 1.0f / (float)(2 * M);
         for (int k = tid; k < M; k += NT)
             bufA[k] = k == 0 ? make_float2(in[0], in[2 * M]) : make_float2(in[2 * k], in[2 * k + 1]);
-        if (tid == 0 && a.status) a.status[blockIdx.x] = (in[1] != 0.f || in[2 * M + 1] != 0.f) ? 1 : 0;
+        // FftError::InputValues: realfft still writes the transform (with the
+        // imaginary parts as 0), and Fft::inverse returns through `?` (:42)
+        // before its normalisation loop (:44-46) -- that row is not scaled
+        const bool bad = in[1] != 0.f || in[2 * M + 1] != 0.f;
+        if (tid == 0 && a.status) a.status[blockIdx.x] = bad ? 1 : 0;
         __syncthreads();
         for (int m = tid; m < M; m += NT) bufB[m] = real_pre<LOG2M, NT>(bufA, m, a.tw);
         __syncthreads();
         const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2M, NT, true>(bufB, bufA, a.tw));
-        for (int j = tid; j < 2 * M; j += NT) out[j] = y[j] * invN;  // (x / N: N is a power of two)
+        const float sc = bad ? 1.0f : invN;
+        for (int j = tid; j < 2 * M; j += NT) out[j] = y[j] * sc;  // (x / N: N is a power of two)
     }
 }
 
@@ -1647,18 +1652,18 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
         const int var = pick_variant(a.pa, channels, LOG2B);
         t.pa.pipe = (var & VARIANT_NOPIPE) ? 0 : 1;  // (the replay path's generic step)
         t.pa.lag = pipeline_lag(LOG2B);
-        hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
-        {
-            constexpr int F = B / 2, FC = F < T0_FC ? F : T0_FC;
-            const size_t lds = tail0_mac_lds<LOG2B>(a.act, a.n);
-            auto mk = tail0_mac_kernel<LOG2B>;
-            if (lds > 160 * 1024 || (256 / FC) * T0_J < a.n) return hipErrorInvalidValue;
-            if (lds > 64 * 1024) {
-                hipError_t e = hipFuncSetAttribute((const void *)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                if (e != hipSuccess) return e;
-            }
-            hipLaunchKernelGGL(mk, dim3(channels, F / FC), dim3(256), lds, s, t);
+        // (every check before the first launch: a failure leaves the pending
+        // blocks and tail0's state untouched)
+        constexpr int F = B / 2, FC = F < T0_FC ? F : T0_FC;
+        const size_t lds = tail0_mac_lds<LOG2B>(a.act, a.n);
+        auto mk = tail0_mac_kernel<LOG2B>;
+        if (lds > 160 * 1024 || (256 / FC) * T0_J < a.n) return hipErrorInvalidValue;
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
         }
+        hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
+        hipLaunchKernelGGL(mk, dim3(channels, F / FC), dim3(256), lds, s, t);
         hipLaunchKernelGGL(tail0_c2r_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
         hipLaunchKernelGGL(tail0_commit_kernel<LOG2B>, dim3(channels, (a.n + KT - 1) / KT), dim3(256), 0, s, t);
         constexpr size_t rep_lds = Geo<LOG2B, NT>::lds_bytes;  // (the generic step)
@@ -1755,7 +1760,7 @@ LaDims la_dims(int log2b, int S) {
     d.nlv = la_nlv(S);
     for (int lv = 1; lv <= 3; ++lv) d.per[lv - 1] = la_per(lv);
     const int nsl = log2b >= 7 ? (1 << (log2b - 1)) / 64 : 1;  // LaGeo::NSL
-    d.wg[0] = log2b <= 8 ? 0 : 1;                               // LaStep::MIDIN: level 1 in the step workgroups
+    d.wg[0] = log2b <= FFTCONV_LA_MIDIN_MAXLOG ? 0 : 1;        // LaStep::MIDIN: level 1 in the step workgroups
     d.wg[1] = nsl * (LA_P2 / LA_JW);
     d.wg[2] = d.nlv == 3 ? nsl * (LA_P3 / LA_JW) : 0;
     d.pt = LA_PT;
@@ -1832,11 +1837,11 @@ hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStre
     FFTCONV_DISPATCH(launch_la_t, log2b, a, channels, s)
 }
 
-int la_trace_grid(int log2b, int S, int channels) {
+int la_trace_grid(int log2b, int S, int channels) {  // (steady-state launches: la_t = 0 has the most anchors)
     if (log2b < 7 || log2b > 9) return 0;
     ProcArgs a{};
-    la_counts(a, log2b, S, channels, true, true);
-    return a.la_n[0] + a.la_n[1] + a.la_n[2] + channels + LA_XWG;
+    la_counts(a, log2b, S, channels, false, true);
+    return 2 * (a.la_n[0] + a.la_n[1] + a.la_n[2]) + channels + LA_XWG;  // (XF 3: A's and B's anchors)
 }
 
 // ---------------------------------------------------------------------------

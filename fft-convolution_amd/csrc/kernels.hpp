@@ -21,6 +21,12 @@ enum : int {
     FLAG_PW2 = 128,
     FLAG_LA3 = 256,
     FLAG_PW3 = 512,
+    // a multi-block call on the lookahead path (ProcJob::mcall > 1) is done
+    // for this channel before its last launch: it ran the whole call by the
+    // generic chunk loop in the first launch (off the lookahead path), or a
+    // block's C2R failed (the call's output is zero-filled, :264-267); the
+    // call's remaining launches skip it, the last one clears the flag
+    FLAG_CALLDONE = 1 << 10,
     SEQ_SHIFT = 24,
     // lookahead: pre[] holds the near rows' sum (rows D0..1) of the block
     // that starts at `current`, left by the previous step (la.hpp)
@@ -65,6 +71,10 @@ struct ProcJob {
     long long tin_stride;
     int S;                 // seg_count (row pitch of H and X in rows)
     int n;                 // output samples this call
+    // lookahead launches of a multi-block call (n = mcall * B, one launch per
+    // block, in / out advanced by mk * B): blocks of the whole call, this
+    // launch's block (0 / 0 otherwise)
+    int mcall, mk;
 };
 
 // Crossfader::mix over one call's samples (src/crossfade_convolver.rs:242-278),

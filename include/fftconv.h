@@ -68,7 +68,9 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
  * Inverse (Fft::inverse :41-49): n/2+1 bins -> n reals divided by n;
  * d_status[row] (optional) = 1 where realfft returns FftError::InputValues
  * (non-zero DC / Nyquist imaginary part; the transform runs with those parts
- * as 0).  Strides in floats; enqueued on `hip_stream` (NULL = legacy stream). */
+ * as 0).  Such a row is NOT divided by n: Fft::inverse returns the error
+ * through `?` (:42) before its normalisation loop (:44-46).  Strides in
+ * floats; enqueued on `hip_stream` (NULL = legacy stream). */
 int fftconv_fft_forward(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
                         size_t out_stride, void *hip_stream);
 int fftconv_fft_inverse(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,

@@ -181,7 +181,11 @@ int oracle_rfft_inverse(size_t n, const float *in, float *x) {
     if (!tmp) { rfft_free(&f); return -1; }
     memcpy(tmp, in, (n / 2 + 1) * sizeof(cpx));
     int bad = rfft_inverse(&f, tmp, x);
-    for (size_t i = 0; i < n; i++) x[i] /= (float)n; /* :44-46 */
+    /* :42 returns FftError::InputValues through `?` before the normalisation
+       loop :44-46 (realfft has written the transform with those imaginary
+       parts as 0), so a flagged row stays unscaled */
+    if (!bad)
+        for (size_t i = 0; i < n; i++) x[i] /= (float)n; /* :44-46 */
     free(tmp);
     rfft_free(&f);
     return bad;

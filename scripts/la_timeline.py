@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Summarise FFTCONV_LA_TRACE launch timelines (csrc/la.hpp upols_la_kernel):
-per role (0 far anchor, 1 mid anchor, 2 step, 4 mix walk) when its waves start
+per role (0 level-3 anchor, 1 level-2 anchor, 2 step, 3 level-1 anchor, 4 mix
+walk; csrc/la.hpp la_role) when its waves start
 and end, relative to the launch's first wave (s_memrealtime ticks, 10 ns)."""
 import sys
 
 import numpy as np
 
-ROLES = {0: "far", 1: "mid", 2: "step", 4: "mixwalk", 5: "pad"}
+ROLES = {0: "level3", 1: "level2", 2: "step", 3: "level1", 4: "mixwalk", 5: "pad"}
 
 
 def load(path):

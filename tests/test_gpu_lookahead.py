@@ -319,3 +319,43 @@ def test_lookahead_three_levels_phase_and_full_sum(amd):
     for c in range(1, C):
         assert np.array_equal(outs[-1][c], outs[-1][0]), c
     assert np.array_equal(outs[-1], outs[LAFULL])
+
+
+@pytest.mark.parametrize("B", [128, 256])
+def test_lookahead_multi_block_calls(amd, oracle_mod, B):
+    """Calls of m whole blocks (src/fft_convolver.rs:222-294 loops over any
+    output.len(); src/tests.rs:119-146 feeds 2B-sample calls to a B-block
+    convolver) stay on the lookahead path: bit-identical to m one-block
+    calls, within tolerance of the oracle -- including a multi-block call
+    that starts with buffered samples (the whole call by the chunk loop),
+    and a non-finite sample in the middle block of a 3-block call (the
+    reference zero-fills the whole call's output and stops, :239-240)."""
+    rng = np.random.default_rng(600 + B)
+    C, L = 6, 150 * B + 17
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    multi = amd.FFTConvolver.init(hs, B, L, channels=C)
+    single = amd.FFTConvolver.init(hs, B, L, channels=C)
+    refs = _refs(oracle_mod, hs, B, L)
+    calls = [B] * 40 + [2 * B] * 30 + [4 * B] * 20 + [3 * B] * 10 + [B // 2] + [2 * B, B // 2] + [B] * 5 + [3 * B] * 4
+    nan_call = len(calls) - 2
+    filled = 0  # samples into the current block before the call
+    for j, n in enumerate(calls):
+        x = np.stack([white(rng, n) for _ in range(C)])
+        if j == nan_call:
+            x[3, B + 7] = np.nan
+        got = multi.process(x)
+        if n % B == 0 and filled == 0 and j < nan_call:
+            one = np.concatenate([single.process(x[:, k * B:(k + 1) * B]) for k in range(n // B)], axis=1)
+            assert np.array_equal(got, one), (j, n)
+        else:
+            # (buffered samples: the reference's chunks of one call differ
+            # from those of m calls, so only the oracle comparison applies)
+            single.process(x)
+        filled = (filled + n) % B
+        for c in range(C):
+            r = refs[c].process(x[c])
+            assert np.array_equal(np.isnan(got[c]), np.isnan(r)), (j, c)
+            m = ~np.isnan(r)
+            assert_close(got[c][m], r[m], what=f"B={B} call {j} (n={n}) ch {c}")
+        for c in range(C):
+            assert multi.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill), (j, c)

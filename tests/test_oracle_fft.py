@@ -30,4 +30,6 @@ def test_rfft_inverse_flags_input_values(oracle_mod):
     Xb = X.copy()
     Xb[-1] += 1j  # non-zero Nyquist imaginary part: realfft's FftError::InputValues
     y2, bad2 = oracle_mod.rfft_inverse(Xb, n)
-    assert bad2 and np.array_equal(y2, y)  # computed with that part taken as 0
+    # computed with that part taken as 0, and not divided by n: Fft::inverse
+    # returns the error through `?` (src/fft_convolver.rs:42) before :44-46
+    assert bad2 and np.array_equal(y2, y * n)
