@@ -1760,7 +1760,7 @@ LaDims la_dims(int log2b, int S) {
     d.nlv = la_nlv(S);
     for (int lv = 1; lv <= 3; ++lv) d.per[lv - 1] = la_per(lv);
     const int nsl = log2b >= 7 ? (1 << (log2b - 1)) / 64 : 1;  // LaGeo::NSL
-    d.wg[0] = log2b <= FFTCONV_LA_MIDIN_MAXLOG ? 0 : 1;        // LaStep::MIDIN: level 1 in the step workgroups
+    d.wg[0] = log2b <= LA_MIDIN_MAXLOG ? 0 : 1;                // LaStep::MIDIN: level 1 in the step workgroups
     d.wg[1] = nsl * (LA_P2 / LA_JW);
     d.wg[2] = d.nlv == 3 ? nsl * (LA_P3 / LA_JW) : 0;
     d.pt = LA_PT;

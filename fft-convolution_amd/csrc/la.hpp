@@ -58,31 +58,16 @@ constexpr int LA_PER = 64;                   // stagger clock modulus (every per
 constexpr int LA_JW = 8;                     // far-style window steps per workgroup (register window)
 constexpr int LA_U = 2;                      // anchor: H / X rows in flight per lane
 constexpr int LA_UF = 2;                     // level 2/3 anchors: H / X rows in flight per lane
-#ifndef FFTCONV_LA_HE
-#define FFTCONV_LA_HE 1
-#endif
-#ifndef FFTCONV_LA_UM
-#define FFTCONV_LA_UM 2
-#endif
-constexpr int LA_UM = FFTCONV_LA_UM;         // level 1 anchors: H / X rows in flight per lane
+constexpr int LA_UM = 4;                     // level 1 anchors: H / X rows in flight per lane
 constexpr int LA_NT = 256;                   // threads per workgroup (anchor and step roles)
 constexpr int LA_NG = 4;                     // row groups of a level 2/3 anchor (one wave each)
 constexpr int LA_CU = 8;                     // full-pass chain: rows in flight per lane
 constexpr int LA_OOB = 0x7ffffff0;           // a buffer voffset past every stream's range
-// launch-shape options (A/B builds): step workgroups ahead of the anchors in
-// the grid; the largest log2 B whose step workgroups run the level-1 anchors
-// (else level-1 anchor workgroups); the smallest log2 B whose helpers store
-// the next block's near sum
-#ifndef FFTCONV_LA_SF
-#define FFTCONV_LA_SF 0
-#endif
-#ifndef FFTCONV_LA_MIDIN_MAXLOG
-#define FFTCONV_LA_MIDIN_MAXLOG 8
-#endif
-#ifndef FFTCONV_LA_NEARNEXT_MINLOG
-#define FFTCONV_LA_NEARNEXT_MINLOG 9
-#endif
-constexpr bool LA_STEPS_FIRST = FFTCONV_LA_SF != 0;
+// launch shape: the largest log2 B whose step workgroups run the level-1
+// anchors (else level-1 anchor workgroups); the smallest log2 B whose helpers
+// store the next block's near sum (round-3 A/Bs)
+constexpr int LA_MIDIN_MAXLOG = 8;
+constexpr int LA_NEARNEXT_MINLOG = 9;
 static_assert(LA_P1 <= LA_D0 && LA_P2 <= LA_R1 && LA_P3 <= LA_R2, "a level's rows are older than its window");
 static_assert(LA_PER % LA_P1 == 0 && LA_PER % LA_P2 == 0 && LA_PER % LA_P3 == 0, "stagger clock");
 static_assert(LA_P2 % LA_JW == 0 && LA_P3 % LA_JW == 0 && LA_P1 <= 8, "window slices");
@@ -443,8 +428,8 @@ struct LaStep {
     // after the pre) also run the level-1 anchors of its channels, after the
     // pre, under the transform chains; B = 512 launches level-1 anchor
     // workgroups
-    static constexpr bool MIDIN = LOG2B <= FFTCONV_LA_MIDIN_MAXLOG;
-    static constexpr bool NEARNEXT = LOG2B >= FFTCONV_LA_NEARNEXT_MINLOG;
+    static constexpr bool MIDIN = LOG2B <= LA_MIDIN_MAXLOG;
+    static constexpr bool NEARNEXT = LOG2B >= LA_NEARNEXT_MINLOG;
     // tw (the 3N/4 = 1.5B float2 the transforms index) | per channel:
     // bufA | bufB | pre (float2) | tail0 | tail1 (float) -- H[0] and the
     // overlap stay in the chain wave's registers (XF 3 at B = 512: 38 KB, so
@@ -682,12 +667,8 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         wave_r2c_post<LOG2B>(bufA, bufB, twl, Q, JC.X + c * rows + (size_t)cur * B);
         la_stamp(a, 1);
     } else {
-#if !FFTCONV_LA_HE
         if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
-#endif
-        // ---- pre = near chain (rows D0..1) + (W1 + (W2 + W3)), canonical order.
-        // Issued with the launch: the chain waves' twiddle barrier comes
-        // after it (the pre rows only meet the chains at the barrier below)
+        // ---- pre = near chain (rows D0..1) + (W1 + (W2 + W3)), canonical order
 #pragma unroll
         for (int t = 0; t < TPL; ++t) {
             int k, f;
@@ -731,9 +712,6 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             if constexpr (TPL > 2) __builtin_amdgcn_sched_barrier(0);  // (one task's rows in flight at a time)
         }
         la_stamp(a, 0);
-#if FFTCONV_LA_HE
-        if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
-#endif
     }
     __syncthreads();
     la_stamp(a, 2);
@@ -1086,14 +1064,12 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
         }
     }
     const int nanchor = a.la_n[0] + a.la_n[1] + a.la_n[2];
-    const int nstep = (a.la_channels + NCH - 1) / NCH;
     const int b = (int)blockIdx.x - (XF == 1 ? LA_XWG : 0);
-    const int ba = LA_STEPS_FIRST ? b - nstep : b;  // anchor index (< 0: a step)
-    if (ba >= 0 && ba < nanchor) {
-        la_anchor<LOG2B, NTL>(a, 0, ba, smem);
+    if (b < nanchor) {
+        la_anchor<LOG2B, NTL>(a, 0, b, smem);
         return;
     }
-    const int c0 = (LA_STEPS_FIRST ? b : b - nanchor) * NCH;
+    const int c0 = (b - nanchor) * NCH;
     const ProcJob &J = a.job[0];
     const int nvalid = min(NCH, a.la_channels - c0);
     int cs[NCH];
@@ -1116,7 +1092,7 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
 
 // the role of workgroup blockIdx.x in a lookahead launch (for the timeline):
 // 0 level-3 anchor, 1 level-2 anchor, 2 step, 3 level-1 anchor, 4 mix walk, 5 padding
-template <int XF, int NCH>
+template <int XF>
 __device__ __forceinline__ int la_role(const ProcArgs &a) {
     int b = (int)blockIdx.x;
     if (XF == 3) {
@@ -1131,11 +1107,6 @@ __device__ __forceinline__ int la_role(const ProcArgs &a) {
     if (XF == 1) {
         if (b < LA_XWG) return 4;
         b -= LA_XWG;
-    }
-    if (LA_STEPS_FIRST) {
-        const int nstep = (a.la_channels + NCH - 1) / NCH;
-        if (b < nstep) return 2;
-        b -= nstep;
     }
     if (b < a.la_n[2]) return 0;
     b -= a.la_n[2];
@@ -1157,7 +1128,7 @@ __global__ __launch_bounds__(LA_NT, 4) void upols_la_kernel(ProcArgs a) {
             const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID
             const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
             a.la_trace[(size_t)blockIdx.x * 4 + wave] =
-                make_int4(la_role<XF, LaStep<LOG2B, XF>::NCH>(a) | (wave << 4), (int)((hw & 0xffffu) | ((xcc & 0xffu) << 24)), (int)t0, (int)t1);
+                make_int4(la_role<XF>(a) | (wave << 4), (int)((hw & 0xffffu) | ((xcc & 0xffu) << 24)), (int)t0, (int)t1);
         }
     }
 }

@@ -119,10 +119,18 @@ def cpu_baseline(kind, C, block, L, every=0, target_s=6.0):
                       f"in {secs:.1f}s" + (f", update() every {every} blocks" if every else "")}
 
 
-def pmc_kernels(configs, steps_args):
-    """Median HBM bytes per launch of every kernel of this script's run of
-    `configs` (two separate rocprofv3 --pmc passes, before this process
-    touches the GPU).  Returns {kernel name: bytes} or a note string."""
+PMC_STEPS = {"3": 256, "5": 256, "2u": 256}
+PMC_WARMUP = {"3": 128, "5": 64, "2u": 200}  # (run()'s warmup per config: cfg3 2T/head, cfg5 64, cfg2u 200)
+PMC_REGEX = "upols_|ir_segments|la_rebuild|tail0_|twostage_accum|crossfade_mix|reset_state"
+
+
+def pmc_config(cfg):
+    """HBM traffic of ONE config's run (its own two rocprofv3 --pmc passes,
+    FETCH_SIZE and WRITE_SIZE, before this process touches the GPU): per
+    kernel the median bytes per launch and the launches, and the measured
+    bytes per step -- every dispatch from the config's first process launch
+    on (init and IR upload excluded, the updates inside the timed region
+    included) over the run's warmup + timed calls.  Returns a dict or a note."""
     import csv
     import glob
     import shutil
@@ -134,30 +142,40 @@ def pmc_kernels(configs, steps_args):
     if not prof:
         return "rocprofv3 not found"
     env = dict(os.environ, TMPDIR="/tmp")
-    vals = {}
+    steps_args = [f"--steps{cfg[0] if cfg != '2u' else '2'}", str(PMC_STEPS[cfg])]
+    per = {}    # kernel -> {counter: [values per dispatch]}
+    total = {}  # counter -> bytes from the first process dispatch on
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir="/tmp")
-        cmd = [prof, "--pmc", counter, "--kernel-include-regex", "upols_|ir_segments|la_rebuild", "-d", d, "-o",
-               "pmc", "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--configs", configs,
-               "--no-cpu", "--pmc-inner"] + steps_args
+        cmd = [prof, "--pmc", counter, "--kernel-include-regex", PMC_REGEX, "-d", d, "-o", "pmc", "--output-format",
+               "csv", "--", sys.executable, os.path.abspath(__file__), "--configs", cfg, "--no-cpu",
+               "--pmc-inner"] + steps_args
         try:
             subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            timeout=300, check=True)
         except Exception as e:
             return f"rocprofv3 --pmc {counter} failed: {type(e).__name__}"
-        per = {}
+        rows = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 if r.get("Counter_Name") == counter:
-                    per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+                    rows.append((int(r.get("Dispatch_Id") or r.get("Correlation_Id") or len(rows)), r["Kernel_Name"],
+                                 float(r["Counter_Value"])))
         shutil.rmtree(d, ignore_errors=True)
-        for k, v in per.items():
-            vals.setdefault(k, {})[counter] = statistics.median(v)
-    out = {}
-    for k, v in vals.items():
+        rows.sort()
+        first = next((i for i, r in enumerate(rows) if "upols_" in r[1]), len(rows))
+        scale = 2048 if counter == "FETCH_SIZE" else 1024  # (KB; FETCH_SIZE counts half on gfx950)
+        total[counter] = sum(v for _, _, v in rows[first:]) * scale
+        for _, k, v in rows[first:]:
+            per.setdefault(k, {}).setdefault(counter, []).append(v * scale)
+    calls = PMC_STEPS[cfg] + PMC_WARMUP[cfg]
+    kern = {}
+    for k, v in per.items():
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            out[k] = int(2 * v["FETCH_SIZE"] * 1024 + v["WRITE_SIZE"] * 1024)
-    return out
+            kern[k] = {"bytes_per_launch": int(statistics.median(v["FETCH_SIZE"]) + statistics.median(v["WRITE_SIZE"])),
+                       "launches_per_step": round(len(v["FETCH_SIZE"]) / calls, 4)}
+    return {"kernels": kern, "measured_bytes_per_step": int((total["FETCH_SIZE"] + total["WRITE_SIZE"]) / calls),
+            "calls": calls, "correction": "read = 2 x FETCH_SIZE KB, write = WRITE_SIZE KB (gfx950)"}
 
 
 def main():
@@ -175,9 +193,11 @@ def main():
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--variant", type=int, default=-1, help="fftconv_set_kernel_variant for every config")
     a = p.parse_args()
-    traffic = None
+    traffic = {}
     if a.pmc and not a.pmc_inner:  # (child processes first: this one has not touched the GPU yet)
-        traffic = pmc_kernels(a.configs, ["--steps2", "256", "--steps3", "256", "--steps5", "256"])
+        for cfg in a.configs.split(","):
+            if cfg in PMC_STEPS:
+                traffic[cfg] = pmc_config(cfg)
     F.set_kernel_variant(a.variant)
     torch.cuda.set_device(0)
     s = torch.cuda.Stream()
@@ -207,7 +227,7 @@ def main():
                 t = sorted(ts)[len(ts) // 2]
                 out.append({"config": "cfg3 sweep", "knobs": kn, "MSamples_s": round(samples / t / 1e6, 2),
                             "us_per_step": round(t / a.steps3 * 1e6, 3)})
-        for batched in (False, True):
+        for batched in ((True,) if a.pmc_inner else (False, True)):
             t, ev = run(conv, C, head, head, a.steps3, 2 * T // head, 64, s, batched=batched)
             out.append({"config": "cfg3 TwoStageFFTConvolver", "host_loop": "C++ (process_device_steps)" if batched
                         else "Python (one process_device per step)", "channels": C, "head": head, "tail": T,
@@ -219,7 +239,8 @@ def main():
                         "canonical_bytes_per_sample": round(canon_sample, 1),
                         "path": "head: one fused launch per call; tail0 deferred to the period end (one pass per "
                                 "period); tail: side stream" if tail0_b != uniform_bytes(head, T) else
-                                "head + tail0: one launch per call; tail: side stream"})
+                                "head + tail0: one launch per call; tail: side stream",
+                        "cfg": "3", "model_bytes_per_step": int(per_sample * C * head)})
         del conv
         if not a.no_cpu and not a.pmc_inner:
             out[-1]["cpu_baseline"] = cpu_baseline("twostage", C, head, L)
@@ -250,7 +271,8 @@ def main():
                     "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
                     "bytes_per_sample": round(per_sample, 1),
                     "canonical_bytes_per_sample": round(2 * uniform_bytes(B, L) / B, 1),
-                    "note": "update_device() (HBM-resident IRs: S-segment FFTs per channel) is inside the timed region"})
+                    "note": "update_device() (HBM-resident IRs: S-segment FFTs per channel) is inside the timed region",
+                    "cfg": "5", "model_bytes_per_step": int(per_sample * C * B)})
         del conv, fresh
         if not a.no_cpu and not a.pmc_inner:
             out[-1]["cpu_baseline"] = cpu_baseline("crossfade", C, B, L, every=128)
@@ -295,11 +317,13 @@ def main():
         out.append({"config": "cfg2u FFTConvolver, update_device every 128 blocks", "channels": C, "block": B,
                     "ir": L, "steps": a.steps2, "MSamples_s": round(samples / t / 1e6, 2),
                     "us_per_step": round(t / a.steps2 * 1e6, 3),
-                    "note": "update_device() (IR transform + window rebuild) inside the timed region"})
+                    "note": "update_device() (IR transform + window rebuild) inside the timed region",
+                    "cfg": "2u", "model_bytes_per_step": int(lookahead_bytes_per_channel_block(B, L) * C)})
         del conv, fresh
-    if traffic is not None:
-        for o in out:
-            o["traffic_bytes_per_launch"] = traffic
+    for o in out:
+        t = traffic.get(o.get("cfg"))
+        if t is not None:
+            o["traffic"] = t  # (this config's own PMC passes)
     for o in out:
         print(json.dumps(o), flush=True)
 

@@ -8,4 +8,4 @@ scripts/gpu_step.sh ${tag}_gputest 600 python -u -m pytest tests -m gpu -q --tim
 grep -q " passed" gpurun_out/${tag}_gputest.log && ! grep -q "failed" gpurun_out/${tag}_gputest.log || exit 5
 scripts/gpu_step.sh ${tag}_bench 300 python bench.py || exit $?
 scripts/profile.sh $tag || exit $?
-scripts/gpu_step.sh ${tag}_configs 600 python scripts/bench_configs.py --configs 3,5 --pmc || exit $?
+scripts/gpu_step.sh ${tag}_configs 600 python scripts/bench_configs.py --configs 3,5,2u --pmc || exit $?
