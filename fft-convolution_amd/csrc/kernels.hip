@@ -1777,7 +1777,7 @@ static void la_counts(ProcArgs &a, int log2b, int S, int C, bool all, bool mid_w
         const int P = d.per[lv - 1];
         const int t0 = a.la_t % P;
         const int n = all ? C - a.la_c0 : (C > t0 ? (C - t0 + P - 1) / P : 0);
-        if (lv == 1) a.la_n[0] = mid_wg ? n : 0;
+        if (lv == 1) a.la_n[0] = mid_wg ? (n + 7) / 8 * 8 : 0;  // (whole rounds of 8: the XF 3 grid interleave)
         else a.la_n[lv - 1] = (lv <= d.nlv) ? (n + 7) / 8 * 8 * d.wg[lv - 1] : 0;
     }
     a.la_nlv = d.nlv;

@@ -58,7 +58,11 @@ constexpr int LA_PER = 64;                   // stagger clock modulus (every per
 constexpr int LA_JW = 8;                     // far-style window steps per workgroup (register window)
 constexpr int LA_U = 2;                      // anchor: H / X rows in flight per lane
 constexpr int LA_UF = 2;                     // level 2/3 anchors: H / X rows in flight per lane
-constexpr int LA_UM = 4;                     // level 1 anchors: H / X rows in flight per lane
+// level-1 walks: H / X rows in flight per lane for a window of JM steps per
+// laneset -- 4 where the X ring (JM + U rows) is a whole number of U-row
+// turns (the 4-step in-step walk at B = 256: 16.60 vs 17.19 us per cfg2
+// step with 2, r3), else 2 or 3, so the unrolled ring stays short
+__host__ __device__ constexpr int la_um(int JM) { return JM >= 4 ? 4 : (JM == 2 ? 2 : 3); }
 constexpr int LA_NT = 256;                   // threads per workgroup (anchor and step roles)
 constexpr int LA_NG = 4;                     // row groups of a level 2/3 anchor (one wave each)
 constexpr int LA_CU = 8;                     // full-pass chain: rows in flight per lane
@@ -166,6 +170,27 @@ __device__ __forceinline__ float4 *la_win(const ProcArgs &a, int jb, size_t c, i
     }
 #endif
     return reinterpret_cast<float4 *>((jb ? a.laW2 : a.laW) + (((c * 2 + win) * LA_PT + la_off(lv) + pos) * (size_t)B));
+}
+
+// Crossfade A and B in one launch (XF 3, CrossfadeConvolver::process
+// :72-77): both convolvers see the same input, so while their ring states
+// agree and FLAG_XSYNC says they always have, their FDLs are equal row for
+// row.  B's FDL reads then go to A's copy: A's and B's walkers of a channel run
+// side by side on one XCD (la_kernel_body's XF 3 grid), and the second read
+// of each row is an L2 hit -- one X stream for both windows.  (A state pair
+// seen pre- and post-step simply does not match: B reads its own copy.)
+__device__ __forceinline__ bool la_xf_paired(int4 sa, int4 sb) {
+    return (sa.w & sb.w & FLAG_XSYNC) && sa.x == sb.x && sa.y == sb.y && sa.z == sb.z &&
+           !((sa.w ^ sb.w) & FLAG_INBUF);
+}
+__device__ __forceinline__ const float2 *la_xsrc(const ProcArgs &a, int jb, size_t c) {
+    if (jb == 0 || a.la_mix != 3) return a.job[jb].X;
+    const int4 sa = a.job[0].state[c], sb = a.job[1].state[c];
+    const int4 ua = make_int4(__builtin_amdgcn_readfirstlane(sa.x), __builtin_amdgcn_readfirstlane(sa.y),
+                              __builtin_amdgcn_readfirstlane(sa.z), __builtin_amdgcn_readfirstlane(sa.w));
+    const int4 ub = make_int4(__builtin_amdgcn_readfirstlane(sb.x), __builtin_amdgcn_readfirstlane(sb.y),
+                              __builtin_amdgcn_readfirstlane(sb.z), __builtin_amdgcn_readfirstlane(sb.w));
+    return la_xf_paired(ua, ub) ? a.job[0].X : a.job[1].X;
 }
 
 // ---------------------------------------------------------------------------
@@ -338,7 +363,7 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
     la_group(LV, l, act, lo, hi);
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
-    const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
+    const RowStream hs(J.H + (size_t)c * rows, bytes), xs(la_xsrc(a, jb, (size_t)c) + (size_t)c * rows, bytes);
     LaAcc acc[LA_JW];
 #pragma unroll
     for (int j = 0; j < LA_JW; ++j) acc[j].zero();
@@ -373,20 +398,20 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
 // threads [t0, t0 + L*F).  Used by the level-1 anchor workgroups (B = 512)
 // and by the step workgroups' helper waves (in-step, B <= 256).
 template <int LOG2B, int JM>
-__device__ __forceinline__ void la_level1(const ProcArgs &a, int jb, int c, int cur, int act, int win, int d, int l,
-                                          int f) {
+__device__ __forceinline__ void la_level1(const ProcArgs &a, int jb, const float2 *X, int c, int cur, int act, int win,
+                                          int d, int l, int f) {
     constexpr int B = 1 << LOG2B;
     const ProcJob &J = a.job[jb];
     const int hi = la_hi(1, act);
     if (hi <= LA_D0 + 1) return;
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
-    const RowStream hs(J.H + (size_t)c * rows, bytes), xs(J.X + (size_t)c * rows, bytes);
+    const RowStream hs(J.H + (size_t)c * rows, bytes), xs(X + (size_t)c * rows, bytes);
     const int j0 = la_mid_j0(l, JM);
     LaAcc acc[JM];
 #pragma unroll
     for (int j = 0; j < JM; ++j) acc[j].zero();
-    la_walk<LOG2B, false, false, JM, LA_UM>(acc, hs, xs, f * 16, f == 0, LA_D0 + 1, hi, j0, cur, act);
+    la_walk<LOG2B, false, false, JM, la_um(JM)>(acc, hs, xs, f * 16, f == 0, LA_D0 + 1, hi, j0, cur, act);
 #pragma unroll
     for (int j = 0; j < JM; ++j)
         if (j0 + j >= l * JM && j0 + j < d) la_win(a, jb, c, win, 1, LA_P1 - d + j0 + j, B)[f] = acc[j].get();
@@ -405,7 +430,7 @@ __device__ __forceinline__ void la_anchor_mid(const ProcArgs &a, int jb, int b) 
     const int tid = threadIdx.x;
     const int l = __builtin_amdgcn_readfirstlane(tid / F), f = tid % F;
     if (l * JM >= LA_P1) return;  // (more lanesets than window steps)
-    la_level1<LOG2B, JM>(a, jb, c, cur, act, win, d, l, f);
+    la_level1<LOG2B, JM>(a, jb, la_xsrc(a, jb, (size_t)c), c, cur, act, win, d, l, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -518,6 +543,10 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     // of one channel; otherwise every slot is a channel of job 0
     auto JK = [&](int k) -> const ProcJob & { return (XF == 3 && k == 1) ? a.job[1] : J; };
     auto JB = [&](int k) { return (XF == 3 && k == 1) ? 1 : 0; };
+    // the FDL the helpers read for slot k (XF 3: B's rows from A's copy when
+    // the two are in step, la_xf_paired)
+    const bool xpair = XF == 3 && la_xf_paired(st[0], st[NCH - 1]);
+    auto XK = [&](int k) -> const float2 * { return (XF == 3 && k == 1 && xpair) ? a.job[0].X : JK(k).X; };
     // XF 3: A's / B's block and the mix_value walk in LDS (the two-stage add
     // buffers, unused by a crossfade), and the mix's arrival counter
     float *yA = reinterpret_cast<float *>(chan_lds(0) + 24 * (size_t)B), *yB = yA + B;
@@ -541,9 +570,12 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     for (int k = 0; k < NCH; ++k) anyfull |= k < nvalid && (full(k, 1) || full(k, 2) || full(k, 3));
 
     // helper slot t of this lane: channel k, slot f (valid if k < nvalid)
+    // (F is a multiple of 64 for B >= 128: k is wave-uniform; kept in an SGPR
+    // where a lane has more than two tasks -- at two, the scheduler would then
+    // overlap both tasks' rows and spill)
     auto task = [&](int t, int &k, int &f) {
         const int idx = (tid - 64 * NCH) + t * HL;
-        k = idx / F;
+        k = TPL > 2 ? __builtin_amdgcn_readfirstlane(idx / F) : idx / F;
         f = idx - k * F;
         return idx < NCH * F && k < nvalid;
     };
@@ -676,7 +708,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             const size_t c = (size_t)CS(k);
             const int cur = ST(k).x, act = ST(k).y, flags = ST(k).w;
             const bool nearp = (flags & FLAG_NEAR) != 0;  // the previous step left this block's near sum
-            const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
+            const RowStream hs(JK(k).H + c * rows, bytes), xs(XK(k) + c * rows, bytes);
             float4 hv[LA_D0], xv[LA_D0], N0;
             if (nearp) {
                 N0 = reinterpret_cast<const float4 *>(JK(k).pre + c * B)[f];
@@ -743,7 +775,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 if (!task(t, k, f) || !near_next(k)) continue;
                 const size_t c = (size_t)CS(k);
                 const int cur = ST(k).x, act = ST(k).y;
-                const RowStream hs(JK(k).H + c * rows, bytes), xs(JK(k).X + c * rows, bytes);
+                const RowStream hs(JK(k).H + c * rows, bytes), xs(XK(k) + c * rows, bytes);
                 float4 hv[LA_D0], xv[LA_D0 - 1];
 #pragma unroll
                 for (int i = LA_D0; i >= 1; --i) {
@@ -781,7 +813,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                     const int act = __builtin_amdgcn_readfirstlane(ST(k).y);
                     const int flags = __builtin_amdgcn_readfirstlane(ST(k).w);
                     const int win = (flags & FLAG_PW1) ? 0 : 1, d = la_dnew(c, a, LA_P1);
-                    la_level1<LOG2B, JMS>(a, JB(k), c, cur, act, win, d, l, f);
+                    la_level1<LOG2B, JMS>(a, JB(k), XK(k), c, cur, act, win, d, l, f);
                 }
             }
         }
@@ -943,6 +975,17 @@ __device__ __attribute__((noinline)) void la_fallback_xf(const ProcArgs *ap, int
     __syncthreads();
     process_job<LOG2B, LA_NT, false, NTL>(a, Jb, (size_t)c, sb, smem);
     __syncthreads();
+    if (threadIdx.x == 0) {
+        // (thread 0 stored both states) the rings have diverged -- a C2R
+        // error in one of them: the FDLs differ from here on, never pair again
+        int4 ta = Ja.state[c], tb = Jb.state[c];
+        if (!(ta.x == tb.x && ta.y == tb.y && ta.z == tb.z && !((ta.w ^ tb.w) & FLAG_INBUF))) {
+            ta.w &= ~FLAG_XSYNC;
+            tb.w &= ~FLAG_XSYNC;
+            Ja.state[c] = ta;
+            Jb.state[c] = tb;
+        }
+    }
     float *t = reinterpret_cast<float *>(smem);
     if (m.approaching) {
         if (threadIdx.x == 0) {
@@ -1031,7 +1074,9 @@ __device__ __forceinline__ void la_kernel_body(const ProcArgs &a, unsigned char 
             for (int lv = 3; lv >= 1; --lv) {
                 const int n = a.la_n[lv - 1];
                 if (b < 2 * n) {
-                    const int jb = b >= n ? 1 : 0, ba = b - jb * n;
+                    // A's and B's workgroup of the same anchor slice 8 apart:
+                    // on one XCD, at the same time (la_xsrc: B reads A's rows)
+                    const int jb = (b >> 3) & 1, ba = ((b >> 4) << 3) | (b & 7);
                     if (lv == 3) la_anchor_far<LOG2B, 3, NTL>(a, jb, ba, smem);
                     else if (lv == 2) la_anchor_far<LOG2B, 2, NTL>(a, jb, ba, smem);
                     else la_anchor_mid<LOG2B>(a, jb, ba);
