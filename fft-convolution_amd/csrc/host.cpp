@@ -294,14 +294,17 @@ struct UniformCore {
         if (la_W) {
             const LaDims d = la_dims(log2b, (int)S);
             if (int r = laW.alloc(C * 2 * (size_t)d.pt * B)) return r;
-            if (const char *e = getenv("FFTCONV_LA_TRACE")) {
-                trace_slots = (size_t)std::max(0, atoi(e));
-                trace_grid = (size_t)la_trace_grid(log2b, (int)S, (int)C);
-                if (trace_slots) {
-                    if (int r = trace.alloc(trace_slots * trace_grid * 8)) return r;
-                    HIP_TRY(hipMemset(trace.p, 0, trace.bytes()));
-                    trace_meta.assign(2 * trace_slots, -1);
-                }
+        }
+        // launch timelines (tuning only): FFTCONV_LA_TRACE for the lookahead
+        // launches of a batch that has them, FFTCONV_PROC_TRACE for the
+        // process launches of one that has not (e.g. cfg3's head)
+        if (const char *e = getenv(la_W ? "FFTCONV_LA_TRACE" : "FFTCONV_PROC_TRACE")) {
+            trace_slots = (size_t)std::max(0, atoi(e));
+            trace_grid = la_W ? (size_t)la_trace_grid(log2b, (int)S, (int)C) : C;
+            if (trace_slots) {
+                if (int r = trace.alloc(trace_slots * trace_grid * 8)) return r;
+                HIP_TRY(hipMemset(trace.p, 0, trace.bytes()));
+                trace_meta.assign(2 * trace_slots, -1);
             }
         }
         // twiddles W_N^k in double, rounded to f32
@@ -465,14 +468,18 @@ struct UniformCore {
         a.la_all = la_all ? 1 : 0;
         a.la_t = (int)(la_t % (unsigned long long)la_dims(log2b, (int)S).per_all);  // (every period divides it)
         a.la_seq = la_seq;
-        if (trace_slots && !la_all) {  // (steady-state launches only: the record is sized for them)
-            const size_t slot = (size_t)(la_t % trace_slots);
-            a.la_trace = trace.p + slot * trace_grid * 8;
-            a.la_trace_grid = (int)trace_grid;
-            trace_meta[2 * slot] = (long long)la_t;
-            trace_meta[2 * slot + 1] = -1;  // (grid: the analysis counts the records)
-            HIP_TRY(hipMemsetAsync(a.la_trace, 0, trace_grid * 8 * sizeof(int4), s));
-        }
+        if (!la_all) return trace_fill(a, s);  // (steady-state launches only: the record is sized for them)
+        return FFTCONV_OK;
+    }
+    // this launch's timeline record (slot = launch count mod trace_slots)
+    int trace_fill(ProcArgs &a, hipStream_t s) {
+        if (!trace_slots) return FFTCONV_OK;
+        const size_t slot = (size_t)(la_t % trace_slots);
+        a.la_trace = trace.p + slot * trace_grid * 8;
+        a.la_trace_grid = (int)trace_grid;
+        trace_meta[2 * slot] = (long long)la_t;
+        trace_meta[2 * slot + 1] = -1;  // (grid: the analysis counts the records)
+        HIP_TRY(hipMemsetAsync(a.la_trace, 0, trace_grid * 8 * sizeof(int4), s));
         return FFTCONV_OK;
     }
     void la_advance() {
@@ -516,6 +523,10 @@ struct UniformCore {
             return FFTCONV_OK;
         }
         if (la_W) la_all = true;  // this launch drops every window
+        if (trace_slots && !la_W && n == B) {  // (process timelines: one-block calls)
+            if (int r = trace_fill(a, s)) return r;
+            ++la_t;
+        }
         HIP_TRY(launch_process(log2b, a, (int)C, s));
         return FFTCONV_OK;
     }
@@ -821,6 +832,10 @@ struct TwoStageCore {
                 a.njobs = 2;
             }
             a.tw = head->tw.p;
+            if (head->trace_slots && !head->la_W) {  // (FFTCONV_PROC_TRACE timelines)
+                if (int r = head->trace_fill(a, s)) return r;
+                ++head->la_t;
+            }
             HIP_TRY(launch_process(head->log2b, a, (int)C, s));
             if (defer_block) {  // (counted once the head launch that writes its tail_input is enqueued)
                 if (t0_n == 0) t0_off = tail_input_fill;

@@ -46,9 +46,14 @@ struct Geo {
     static constexpr size_t gen_bytes = ((2 * (size_t)B * sizeof(float2) + red_bytes + tw_bytes + pre_bytes + 15) / 16) * 16;
     // pipelined full-block step (pipelined_step): bufA | bufB | tw (2B) | H0 | H1 | pre | overlap | tail0 | tail1
     static constexpr bool PIPE = LOG2B >= 1 && LOG2B <= 9 && NT == 256;
-    // (the closing reduction reuses the front: 4 waves x 64 lanes x 16 B x slots/lane)
+    // the next block's pre is reduced and stored while the chain runs its C2R
+    // (B <= 256): the reduction slots (4 waves x 64 lanes x 16 B x slots/lane)
+    // after the chain's buffers; at B = 512 they reuse the front once the
+    // chain is done (the process kernel's LDS stays below 40 KB there)
+    static constexpr bool PIPE_EARLY = LOG2B <= 8;
     static constexpr size_t pipe_red = 4 * 64 * 16 * (size_t)(B >= 128 ? B / 128 : 1);
-    static constexpr size_t pipe_bytes = PIPE ? (68 * (size_t)B > pipe_red ? 68 * (size_t)B : pipe_red) : 0;
+    static constexpr size_t pipe_bytes =
+        PIPE ? (PIPE_EARLY ? 68 * (size_t)B + pipe_red : (68 * (size_t)B > pipe_red ? 68 * (size_t)B : pipe_red)) : 0;
     static constexpr size_t lds_bytes = (gen_bytes > pipe_bytes ? gen_bytes : pipe_bytes) + 16;
 };
 
@@ -350,19 +355,24 @@ __device__ __forceinline__ void mac_rows_range(AccArr &acc, const float2 *Hc, co
     const size_t bytes = (size_t)S * ROWB;
     const RowStream hs(Hc, bytes), xs(Xc, bytes);
     const int lane_off = f0 * 16;
+    constexpr int OOB = 0x7ffffff0;  // a voffset past the stream: the load returns 0, no memory access
     int t = t_begin + sw * RPW + rsub;
     int i = 2 + t;
     int xi = (curp + i) % act;
-    for (; t + (U - 1) * STEP < t_end; t += U * STEP) {
+    // batches of U rows, the last one partial: rows past t_end are loaded from
+    // the out-of-range offset and not accumulated, so the last rows of a walk
+    // are in flight together instead of one round trip each (cfg3 head, r3)
+    for (; t < t_end; t += U * STEP) {
         float4 hv[U][SPL], xv[U][SPL];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int ho = i * ROWB, xo = xi * ROWB;
+            const bool in = t + u * STEP < t_end;
+            const int ho = in ? i * ROWB : 0, xo = in ? xi * ROWB : 0;
 #pragma unroll
             for (int s = 0; s < SPL; ++s) {
-                const int lo = lane_off + s * 64 * 16;
-                hv[u][s] = UNIFORM ? hs.ld4<NTL>(lo, ho) : hs.ld4<NTL>(lo + ho, 0);
-                xv[u][s] = UNIFORM ? xs.ld4<NTL>(lo, xo) : xs.ld4<NTL>(lo + xo, 0);
+                const int lo = in ? lane_off + s * 64 * 16 : OOB;
+                hv[u][s] = UNIFORM ? hs.ld4<NTL>(lo, ho) : hs.ld4<NTL>(in ? lo + ho : OOB, 0);
+                xv[u][s] = UNIFORM ? xs.ld4<NTL>(lo, xo) : xs.ld4<NTL>(in ? lo + xo : OOB, 0);
             }
             i += STEP;
             xi += STEP;
@@ -370,21 +380,19 @@ __device__ __forceinline__ void mac_rows_range(AccArr &acc, const float2 *Hc, co
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
+            if (t + u * STEP < t_end) {
 #pragma unroll
-            for (int s = 0; s < SPL; ++s) acc[s].mac(hv[u][s], xv[u][s]);
+                for (int s = 0; s < SPL; ++s) acc[s].mac(hv[u][s], xv[u][s]);
+            }
     }
-    for (; t < t_end; t += STEP) {
-        const int ho = i * ROWB, xo = xi * ROWB;
-#pragma unroll
-        for (int s = 0; s < SPL; ++s) {
-            const int lo = lane_off + s * 64 * 16;
-            const float4 h = UNIFORM ? hs.ld4<NTL>(lo, ho) : hs.ld4<NTL>(lo + ho, 0);
-            const float4 x = UNIFORM ? xs.ld4<NTL>(lo, xo) : xs.ld4<NTL>(lo + xo, 0);
-            acc[s].mac(h, x);
-        }
-        i += STEP;
-        xi += STEP;
-        if (xi >= act) xi -= act;
+}
+
+// launch timeline phase stamp k (0..3) of this wave of a process launch
+// (FFTCONV_PROC_TRACE; job 0 only)
+__device__ __forceinline__ void proc_stamp(const ProcArgs &a, int k) {
+    if (a.la_trace && blockIdx.y == 0 && (threadIdx.x >> 6) < 4 && (threadIdx.x & 63) == 0) {
+        int *p = reinterpret_cast<int *>(a.la_trace + ((size_t)a.la_trace_grid * 4 + (size_t)blockIdx.x * 4 + (threadIdx.x >> 6)));
+        p[k] = (int)(unsigned)__builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -402,6 +410,11 @@ __device__ __forceinline__ void mac_rows_range(AccArr &acc, const float2 *Hc, co
 // so the latency chain hides under the FDL stream instead of following it
 // (lag ~ the chain's duration in rows of stream; set by the host).
 // The next block's pre is reduced in a fixed order and stored (FLAG_PRE).
+// B <= 256 (PIPE_EARLY): the chain parks its share of that pre right after
+// the conv (row 1 needs only the new spectrum) and the helper waves, long
+// done with their rows, reduce and store it and the state word while the
+// chain runs its C2R -- the reduction leaves the launch's critical path
+// (cfg3 head timeline, profiles/r3: it ran after the chain, 0.5 of 5.5 us).
 // ---------------------------------------------------------------------------
 template <int LOG2B, int NT, bool NTL>
 __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob &J, size_t c, int cur, int act,
@@ -421,6 +434,8 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     float *p0l = ovl + B;
     float *p1l = p0l + B;
     int &s_err = *reinterpret_cast<int *>(smem + Gm::lds_bytes - 16);
+    // the next block's pre: partial sums [wave][slot/64][lane]
+    float4 *red = reinterpret_cast<float4 *>(Gm::PIPE_EARLY ? reinterpret_cast<unsigned char *>(p1l + B) : smem);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -451,6 +466,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
+        proc_stamp(a, 0);
         if (J.tin) {  // two-stage: append the block to tail_input (:459-461)
             const float *xb = reinterpret_cast<const float *>(bufA);
             float *ti = J.tin + c * J.tin_stride;
@@ -482,7 +498,20 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             }
         }
         const bool err = __ballot(bad) != 0ull;
+        if constexpr (Gm::PIPE_EARLY) {
+            // the chain's share of the next block's pre (row 1, and the last
+            // w0 rows with a pipeline lag) to the reduction slots; the helper
+            // waves reduce and store it, and the state, during the C2R below
+            const int R = act > 2 ? act - 2 : 0;
+            const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
+            if (w0 > 0) mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, R - w0, R, 1, 0, rsub, f0);
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) red[s * 64 + lane] = acc[s].get(f0 + s * 64);
+            if (lane == 0) s_err = err ? 1 : 0;
+            __syncthreads();  // (B1, the helpers' barrier below)
+        }
         wave_sync();
+        proc_stamp(a, 1);
         if (!err) {
             for (int m = lane; m < B; m += 64) Q[m] = real_pre<LOG2B, 64>(Z, m, twl);
             wave_sync();
@@ -510,7 +539,34 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
                 ibc[j] = inc[j];
             }
         }
-        if (lane == 0) s_err = err ? 1 : 0;
+        if (!Gm::PIPE_EARLY && lane == 0) s_err = err ? 1 : 0;
+        if constexpr (Gm::PIPE_EARLY) return;
+    }
+    if constexpr (Gm::PIPE_EARLY) {
+        // ---- helper waves: FDL rows 2..act-1 - w0 of the next block's pre,
+        // then (B1: the chain's share is in the slots) its fixed-order
+        // reduction and the state, while the chain runs its C2R ----
+        const int R = act > 2 ? act - 2 : 0;
+        const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
+        mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R - w0, NSW, wave - 1, rsub, f0);
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) red[(wave * SPL + s) * 64 + lane] = acc[s].get(f0 + s * 64);
+        proc_stamp(a, 2);
+        __syncthreads();  // (B1)
+        const int ht = tid - 64;
+        if (s_err) {
+            if (ht == 0) J.state[c] = make_int4(cur, act, 0, la_clear(flags | FLAG_INBUF, a));
+            return;
+        }
+        for (int f = ht; f < F; f += NT - 64) {
+            float4 p = red[f];
+            for (int w = 0; w <= NSW; ++w)
+                for (int r = (w == 0 ? 1 : 0); r < RPW; ++r) p = vadd(p, red[w * SPL * 64 + f + r * F]);
+            reinterpret_cast<float4 *>(prec)[f] = p;
+        }
+        if (ht == 0) J.state[c] = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
+        proc_stamp(a, 3);
+        return;
     }
     // ---- FDL rows 2..act-1 of the next block's pre: waves 1..NSW take
     // t in [0, R0), wave 0 (after its chain) the last w0 rows ----
@@ -521,6 +577,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         if (wave == 0) mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, R0, R, 1, 0, rsub, f0);
         else mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R0, NSW, wave - 1, rsub, f0);
     }
+    proc_stamp(a, 2);
     __syncthreads();
     if (s_err) {
         if (tid == 0) J.state[c] = make_int4(cur, act, 0, la_clear(flags | FLAG_INBUF, a));
@@ -529,7 +586,6 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     // next block's pre: every lane parks its partial sums in LDS (the whole
     // workgroup's staging is dead now), then slot f sums waves 0..NSW and
     // sub-rows in a fixed order -- deterministic for a given geometry and lag
-    float4 *red = reinterpret_cast<float4 *>(smem);
 #pragma unroll
     for (int s = 0; s < SPL; ++s) red[(wave * SPL + s) * 64 + lane] = acc[s].get(f0 + s * 64);
     __syncthreads();
@@ -541,6 +597,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         reinterpret_cast<float4 *>(prec)[f] = p;
     }
     if (tid == 0) J.state[c] = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
+    proc_stamp(a, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -796,7 +853,18 @@ __global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const size_t c = blockIdx.x;
     const ProcJob &J = a.job[blockIdx.y];
+    unsigned t0 = 0;
+    if (a.la_trace) t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
     process_job<LOG2B, NT, ZZ, NTL>(a, J, c, J.state[c], smem);
+    if (a.la_trace && blockIdx.y == 0 && (threadIdx.x >> 6) < 4 && (threadIdx.x & 63) == 0) {
+        // launch timeline (FFTCONV_PROC_TRACE, tuning): role 6, as upols_la_kernel's record
+        const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
+        const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID
+        const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+        const int wave = (int)(threadIdx.x >> 6);
+        a.la_trace[(size_t)blockIdx.x * 4 + wave] =
+            make_int4(6 | (wave << 4), (int)((hw & 0xffffu) | ((xcc & 0xffu) << 24)), (int)t0, (int)t1);
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -7,7 +7,7 @@ import sys
 
 import numpy as np
 
-ROLES = {0: "level3", 1: "level2", 2: "step", 3: "level1", 4: "mixwalk", 5: "pad"}
+ROLES = {0: "level3", 1: "level2", 2: "step", 3: "level1", 4: "mixwalk", 5: "pad", 6: "proc"}
 
 
 def load(path):
@@ -43,7 +43,8 @@ def summarise(path):
         wave = (r[:, 0] >> 4) & 15
         for k in np.unique(role):
             for w in (0, 2):  # chain wave / helper wave of the step role
-                m = (role == k) & ((wave >= 2) == (w == 2))
+                nchain = 1 if k == 6 else 2  # (process launch: wave 0 is the chain)
+                m = (role == k) & ((wave >= nchain) == (w == 2))
                 for q in range(4):
                     mm = m & (st[:, q] != 0)
                     if mm.any():
