@@ -122,7 +122,7 @@ int fftconv_set_pipeline_lag(int rows);
 int fftconv_get_pipeline_lag(void);
 
 /* ---- FFTConvolver (uniformly partitioned, zero latency) ---------------- */
-/* FFTConvolver::init, src/fft_convolver.rs:105-186.  NULL on error. */
+/* FFTConvolver::init, src/fft_convolver.rs:105-172.  NULL on error. */
 fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len,
                                       size_t max_block_size, size_t max_response_length);
 /* Batched init on `device`: channel c's response is responses[c*response_stride ..

@@ -8,6 +8,7 @@ import ctypes as C
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fft-convolution_amd"))
@@ -55,18 +56,23 @@ def period(lib, h, y):
 
 
 res = [[] for _ in handles]
+host = [[] for _ in handles]
 for r in range(a.rounds):
     for idx, (lib, h, y) in enumerate(handles):
         period(lib, h, y)  # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
+        t0 = time.perf_counter()
         for _ in range(a.periods):
             period(lib, h, y)
+        t1 = time.perf_counter()
         e1.record(s)
         torch.cuda.synchronize()
         res[idx].append(e0.elapsed_time(e1) * 1000 / (a.periods * steps))
+        host[idx].append((t1 - t0) * 1e6 / (a.periods * steps))
 same = all(torch.equal(handles[0][2], hh[2]) for hh in handles[1:])
-for path, r in zip(a.libs, res):
+for path, r, hr in zip(a.libs, res, host):
     us = statistics.median(r)
-    print(f"{path}: median {us:.3f} us/step (min {min(r):.3f}) -> {Cn * B / us:.1f} MS/s")
+    print(f"{path}: median {us:.3f} us/step (min {min(r):.3f}) -> {Cn * B / us:.1f} MS/s; "
+          f"host enqueue {statistics.median(hr):.3f} us/step")
 print("outputs bit-identical across builds:", same)

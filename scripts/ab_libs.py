@@ -8,6 +8,7 @@ import ctypes as C
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fft-convolution_amd"))
@@ -48,6 +49,7 @@ for spec in a.libs:
     assert h, path
     handles.append((lib, h, torch.empty((16, Cn, B), device="cuda")))
 res = [[] for _ in handles]
+host = [[] for _ in handles]
 k = 0
 for r in range(a.rounds):
     for idx, (lib, h, y) in enumerate(handles):
@@ -71,13 +73,16 @@ for r in range(a.rounds):
         run(20)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
+        t0 = time.perf_counter()
         run(a.steps)
+        host[idx].append((time.perf_counter() - t0) * 1e6 / a.steps)
         e1.record(s)
         k = run.k
         torch.cuda.synchronize()
         res[idx].append(e0.elapsed_time(e1) * 1000 / a.steps)
 same = all(torch.equal(handles[0][2], hh[2]) for hh in handles[1:])
-for path, r in zip(a.libs, res):
+for path, r, hr in zip(a.libs, res, host):
     us = statistics.median(r)
-    print(f"{path}: median {us:.2f} us/step (min {min(r):.2f}) -> {Cn * B / us:.1f} MS/s")
+    print(f"{path}: median {us:.2f} us/step (min {min(r):.2f}) -> {Cn * B / us:.1f} MS/s; "
+          f"host enqueue {statistics.median(hr):.2f} us/step")
 print("outputs bit-identical across builds:", same)

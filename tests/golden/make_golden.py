@@ -64,7 +64,7 @@ def scenarios():
             ops.append(("update", irv(rng, int(rng.integers(1, 2001)))))
         ops.append(("process", white(rng, 512), 512 if i % 3 else 256))
     out["crossfade_512_2000"] = ("crossfade", dict(block=512, max_len=2000), h, ops)
-    # the reference's delta-IR known answer (src/fft_convolver.rs:323-335)
+    # the reference's delta-IR known answer (src/fft_convolver.rs:309-321)
     d = np.zeros(1024, np.float32)
     d[0] = 1.0
     out["uniform_delta_1024"] = ("uniform", dict(block=1024, max_len=1024), d,
