@@ -320,6 +320,21 @@ def main():
                     "note": "update_device() (IR transform + window rebuild) inside the timed region",
                     "cfg": "2u", "model_bytes_per_step": int(lookahead_bytes_per_channel_block(B, L) * C)})
         del conv, fresh
+    if "2m" in a.configs.split(","):
+        # cfg2 with calls of m whole blocks (the reference's process over any
+        # output length, src/fft_convolver.rs:222-294): one lookahead launch per
+        # block, the windows kept -- throughput per m, same per-block work
+        C, B, L = 1024, 256, 48000
+        res = {}
+        for m in (1, 2, 4):
+            conv = F.FFTConvolver.init(shard.synth_irs(range(C), L), B, L, channels=C)
+            nsteps = max(1, a.steps2 // m)
+            t, ev = run(conv, C, m * B, m * B, nsteps, 200 // m, 32 // m, s, batched=True)
+            res[f"calls_of_{m}_blocks"] = {"MSamples_s": round(C * m * B * nsteps / t / 1e6, 2),
+                                           "us_per_block": round(t / (nsteps * m) * 1e6, 3)}
+            del conv
+        out.append({"config": "cfg2m FFTConvolver, calls of m * 256 samples", "channels": C, "block": B, "ir": L,
+                    "per_m": res, "cfg": "2m"})
     for o in out:
         t = traffic.get(o.get("cfg"))
         if t is not None:
