@@ -17,8 +17,11 @@ Multi-GPU (BASELINE configs[3], 8192 channels on 8 GPUs): one process per GPU
 (`--gpus N` without a launcher spawns the N rank processes itself),
 1024 channels per rank (weak scaling, channel shards have no data-path
 exchange); barrier + synchronize around the timed region, max time over ranks.
-`--dry shared` instead broadcasts one dry block per step from rank 0 over RCCL
-(the "one source, many IRs" case) and feeds it to every channel.
+`--dry shared` instead broadcasts the dry blocks from rank 0 over RCCL (the
+"one source, many IRs" case) and feeds each to every channel: one bucketed
+broadcast per run of ring slots (up to `--ring` blocks, 32 KB at the
+default) ahead of that run's process_device_steps call, not one per block
+(`--per-call`: one broadcast and one call per step).
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused
 kernel and `cpu_baseline` from the oracle port on this host (rank 0, N=1).
@@ -302,7 +305,7 @@ def main():
         """k consecutive steps from step i0: one process_device_steps call per
         run of ring slots (the ABI loops over the calls in C++, so Python's
         per-call submission cost stays out of the timed region)."""
-        if args.per_call or args.dry == "shared":
+        if args.per_call:
             for i in range(i0, i0 + k):
                 step(i)
             return
@@ -310,7 +313,13 @@ def main():
         while i < i0 + k:
             r = i % ring
             n = min(ring - r, i0 + k - i)
-            conv.process_device_steps(xin[r].data_ptr(), B, C * B, yout[r].data_ptr(), B, C * B, B, n, sh)
+            if args.dry == "shared":
+                if dist is not None:
+                    shard.broadcast_dry(dist, dry[r:r + n], src=0)  # one collective for the run's n blocks
+                # every channel reads the broadcast block of its step (input stride 0)
+                conv.process_device_steps(dry[r].data_ptr(), 0, B, yout[r].data_ptr(), B, C * B, B, n, sh)
+            else:
+                conv.process_device_steps(xin[r].data_ptr(), B, C * B, yout[r].data_ptr(), B, C * B, B, n, sh)
             i += n
 
     steps(0, args.warmup)
@@ -385,7 +394,7 @@ def main():
                 "segments": S,
                 "dry_input": args.dry,
                 "parallelism": f"channel-shard x{world}",
-                "submission": "per-call" if args.per_call or args.dry == "shared" else "process_device_steps",
+                "submission": "per-call" if args.per_call else "process_device_steps",
             },
             "roofline": {
                 "bound": "hbm",

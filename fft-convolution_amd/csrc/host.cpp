@@ -161,6 +161,13 @@ struct StreamOrder {
 // response into it and returns once the H2D copy and the IR transform are
 // enqueued (the next call on the handle is ordered behind them).  Reserved at
 // init, so update() never allocates (src/lib.rs:8); `busy` guards its reuse.
+// The reservation is capped by fftconv_set_host_stage_limit, and a failed one
+// falls back to smaller sizes (down to one response row): then an
+// update streams its rows through the stage in chunks, each chunk waiting for
+// the previous one's copy out of it -- still no allocation, but the host
+// waits for all but the last chunk's DMA.
+static size_t g_stage_limit = 0;  // bytes, 0 = none
+
 struct PinnedStage {
     float *p = nullptr;
     size_t n = 0;
@@ -176,9 +183,18 @@ struct PinnedStage {
         }
         if (p) (void)hipHostFree(p);
     }
-    int alloc(size_t count) {
+    // count floats wanted, at least min_count (one response row)
+    int alloc(size_t count, size_t min_count) {
         if (count == 0) return FFTCONV_OK;
-        hipError_t e = hipHostMalloc((void **)&p, count * sizeof(float), hipHostMallocDefault);
+        min_count = std::max<size_t>(1, std::min(min_count, count));
+        if (g_stage_limit) count = std::max(min_count, std::min(count, g_stage_limit / sizeof(float)));
+        hipError_t e = hipErrorOutOfMemory;
+        for (;;) {
+            e = hipHostMalloc((void **)&p, count * sizeof(float), hipHostMallocDefault);
+            if (e == hipSuccess || count == min_count) break;
+            (void)hipGetLastError();
+            count = std::max(min_count, count / 4);
+        }
         if (e != hipSuccess) {
             p = nullptr;
             return fail(FFTCONV_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
@@ -198,11 +214,22 @@ struct PinnedStage {
         pending = true;
         return FFTCONV_OK;
     }
-    // channel c of the caller's responses (src + c*stride, len samples) to
-    // rows of `row` floats; stride 0 = one response for every channel (1 row)
-    void fill(const float *src, size_t nch, size_t len, size_t stride, size_t row) {
-        const size_t rows = stride == 0 ? 1 : nch;
-        for (size_t c = 0; c < rows; ++c) std::memcpy(p + c * row, src + c * stride, len * sizeof(float));
+    // rows r of the caller's responses (src + r*stride, len floats each) to
+    // device rows dst + r*dpitch, in as few chunks of whole rows as the stage
+    // holds (one when it was reserved for the whole batch)
+    int upload(const float *src, size_t rows, size_t len, size_t stride, float *dst, size_t dpitch, hipStream_t s) {
+        if (len == 0 || rows == 0) return FFTCONV_OK;
+        if (!p || n < len) return fail(FFTCONV_E_INVALID, "no host staging for this update");
+        const size_t per = n / len;
+        for (size_t r0 = 0; r0 < rows; r0 += per) {
+            const size_t k = std::min(per, rows - r0);
+            if (int r = acquire()) return r;
+            for (size_t c = 0; c < k; ++c) std::memcpy(p + c * len, src + (r0 + c) * stride, len * sizeof(float));
+            HIP_TRY(hipMemcpy2DAsync(dst + r0 * dpitch, dpitch * sizeof(float), p, len * sizeof(float),
+                                     len * sizeof(float), k, hipMemcpyHostToDevice, s));
+            if (int r = release(s)) return r;
+        }
+        return FFTCONV_OK;
     }
 };
 
@@ -289,7 +316,7 @@ struct UniformCore {
         if (int r = tw.alloc(2 * B)) return r;
         if (int r = staging.alloc(C * ir_len)) return r;  // update() never allocates
         if (own_stage)
-            if (int r = hstage.alloc(C * ir_len)) return r;
+            if (int r = hstage.alloc(C * ir_len, ir_len)) return r;
         la_W = la_ok ? la_parts(log2b, (int)S) : 0;
         if (la_W) {
             const LaDims d = la_dims(log2b, (int)S);
@@ -407,24 +434,18 @@ struct UniformCore {
         // and the transform are enqueued behind the handle's previous work,
         // and every later call is ordered behind them (StreamOrder)
         if (int r = order.enter(stream)) return r;
-        return update_host_on(chan0, nch, src, len, stride, stream, hstage, ir_len);
+        return update_host_on(chan0, nch, src, len, stride, stream, hstage);
     }
     // (the caller has ordered stream s behind the handle's previous work);
-    // the response goes through `stage`, rows of `row` >= len floats
+    // the response goes through `stage` into the staging rows
     int update_host_on(size_t chan0, size_t nch, const float *src, size_t len, size_t stride, hipStream_t s,
-                       PinnedStage &stage, size_t row) {
+                       PinnedStage &stage) {
         if (len > ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
         if (ir_len == 0) return FFTCONV_OK;
-        const size_t sst = (stride == 0 && nch > 1) ? 0 : ir_len;
-        if (len && nch) {
-            if (len > row || stage.n < (sst ? nch : 1) * row)
-                return fail(FFTCONV_E_INVALID, "no host staging for this update");
-            if (int r = stage.acquire()) return r;
-            stage.fill(src, nch, len, stride == 0 && nch > 1 ? 0 : stride, row);
-            if (int r = upload(chan0, sst ? nch : 1, stage.p, len, row, s)) return r;
-            if (int r = stage.release(s)) return r;
-        }
-        return ir_from_device(chan0, nch, staging.p + chan0 * ir_len, sst, len, len, true, s);
+        const bool shared = stride == 0 && nch > 1;  // one response for every channel: one staging row
+        if (len && nch)
+            if (int r = stage.upload(src, shared ? 1 : nch, len, stride, staging.p + chan0 * ir_len, ir_len, s)) return r;
+        return ir_from_device(chan0, nch, staging.p + chan0 * ir_len, shared ? 0 : ir_len, len, len, true, s);
     }
 
     // update() from device samples, stream-ordered (used by the crossfade swap)
@@ -576,7 +597,7 @@ struct UniformCore {
         if (int r = staging.alloc(o.staging.n)) return r;
         own_stage = with_stage && o.own_stage;
         if (own_stage)
-            if (int r = hstage.alloc(o.hstage.n)) return r;
+            if (int r = hstage.alloc(o.hstage.n, ir_len)) return r;
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -1070,7 +1091,7 @@ struct CrossfadeCore {
         if (int r = stored.alloc(C * stored_len)) return r;
         if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), stream));
         stage_row = std::max(stored_len, a->ir_len);
-        if (int r = hstage.alloc(C * stage_row)) return r;
+        if (int r = hstage.alloc(C * stage_row, stage_row)) return r;
         xf.init(crossfade_samples, std::min(mbs, max_response_length));
         max_buffer_size = mbs;
         if (int r = buf_a.alloc(C * mbs)) return r;
@@ -1159,7 +1180,7 @@ struct CrossfadeCore {
         if (!is_crossfading()) {
             UniformCore &t = xf.target == 0 ? *b : *a;
             if (len > t.ir_len) return fail(FFTCONV_E_INVALID, "New impulse response is longer than initialized length");
-            if (int r = t.update_host_on(0, C, src, len, stride, stream, hstage, stage_row)) return r;
+            if (int r = t.update_host_on(0, C, src, len, stride, stream, hstage)) return r;
             note_update(xf.target == 0 ? 1 : 0, len);
             xf.fade_into(xf.target == 0 ? 1 : 0);
             response_pending = false;
@@ -1169,18 +1190,9 @@ struct CrossfadeCore {
         // stored_response[..len] = response; stored_response[len..] = 0
         if (stored.n) HIP_TRY(hipMemsetAsync(stored.p, 0, stored.bytes(), stream));
         if (len) {
-            if (int r = hstage.acquire()) return r;
             const bool shared = stride == 0 || C == 1;
-            hstage.fill(src, C, len, shared ? 0 : stride, stored_len);
-            if (shared) {
-                HIP_TRY(hipMemcpyAsync(stored.p, hstage.p, len * sizeof(float), hipMemcpyHostToDevice, stream));
-                stored_stride = C == 1 ? stored_len : 0;
-            } else {
-                HIP_TRY(hipMemcpy2DAsync(stored.p, stored_len * sizeof(float), hstage.p, stored_len * sizeof(float),
-                                         len * sizeof(float), C, hipMemcpyHostToDevice, stream));
-                stored_stride = stored_len;
-            }
-            if (int r = hstage.release(stream)) return r;
+            if (int r = hstage.upload(src, shared ? 1 : C, len, stride, stored.p, stored_len, stream)) return r;
+            stored_stride = shared ? (C == 1 ? stored_len : 0) : stored_len;
         }
         response_pending = true;
         return FFTCONV_OK;
@@ -1353,7 +1365,7 @@ struct CrossfadeCore {
         if (int r = mix_tab.alloc(o.mix_tab.n)) return r;
         if (int r = stored.alloc(o.stored.n)) return r;
         stage_row = o.stage_row;
-        if (int r = hstage.alloc(o.hstage.n)) return r;
+        if (int r = hstage.alloc(o.hstage.n, stage_row)) return r;
         if (stored.n) HIP_TRY(hipMemcpyAsync(stored.p, o.stored.p, stored.bytes(), hipMemcpyDeviceToDevice, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
@@ -1512,6 +1524,11 @@ int fftconv_set_pipeline_lag(int rows) {
     return FFTCONV_OK;
 }
 int fftconv_get_pipeline_lag(void) { return get_pipeline_lag(); }
+int fftconv_set_host_stage_limit(size_t bytes) {
+    g_stage_limit = bytes;
+    return FFTCONV_OK;
+}
+size_t fftconv_get_host_stage_limit(void) { return g_stage_limit; }
 
 // ---- uniform --------------------------------------------------------------
 fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len, size_t max_block_size,

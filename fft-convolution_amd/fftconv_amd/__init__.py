@@ -50,6 +50,8 @@ SIGNATURES = {
     "fftconv_get_kernel_variant": (_i, []),
     "fftconv_set_pipeline_lag": (_i, [_i]),
     "fftconv_get_pipeline_lag": (_i, []),
+    "fftconv_set_host_stage_limit": (_i, [_sz]),
+    "fftconv_get_host_stage_limit": (_sz, []),
     "fftconv_uniform_init": (_vp, [_fp, _sz, _sz, _sz]),
     "fftconv_uniform_init_batch": (_vp, [_i, _sz, _fp, _sz, _sz, _sz, _sz]),
     "fftconv_uniform_update": (_i, [_vp, _fp, _sz]),
@@ -188,6 +190,16 @@ def set_kernel_variant(v: int):
 
 def get_kernel_variant() -> int:
     return int(lib().fftconv_get_kernel_variant())
+
+
+def set_host_stage_limit(nbytes: int):
+    """Cap (bytes, 0 = none) on the pinned host staging a handle reserves at
+    creation for update(); larger updates stream through it in chunks."""
+    _check(lib().fftconv_set_host_stage_limit(nbytes))
+
+
+def get_host_stage_limit() -> int:
+    return int(lib().fftconv_get_host_stage_limit())
 
 
 def set_pipeline_lag(rows: int):

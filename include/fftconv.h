@@ -120,6 +120,17 @@ int fftconv_get_kernel_variant(void);
  * f32 summation order. */
 int fftconv_set_pipeline_lag(int rows);
 int fftconv_get_pipeline_lag(void);
+/* Pinned host staging of update() (process-wide, read when a handle is
+ * created).  A standalone FFTConvolver batch, and a crossfade, reserve
+ * channels x max_response_length floats of pinned host memory at init, so
+ * update() copies the response and returns without waiting for the upload
+ * (src/lib.rs:8 asks update to be real-time safe: it never allocates).  A cap
+ * in bytes (0 = none, the default) -- or a reservation the host refuses, which
+ * falls back to smaller ones down to one response row -- makes update() stream
+ * the rows through the stage in chunks, waiting for each chunk's copy before
+ * refilling it: no allocation either way, same results. */
+int fftconv_set_host_stage_limit(size_t bytes);
+size_t fftconv_get_host_stage_limit(void);
 
 /* ---- FFTConvolver (uniformly partitioned, zero latency) ---------------- */
 /* FFTConvolver::init, src/fft_convolver.rs:105-172.  NULL on error. */

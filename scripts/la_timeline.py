@@ -72,4 +72,7 @@ def summarise(path):
 
 if __name__ == "__main__":
     for p in sys.argv[1:]:
-        print(summarise(p))
+        try:
+            print(summarise(p))
+        except (ValueError, OverflowError) as e:  # (a record from a handle with no traced launches)
+            print(f"{p}: unreadable record ({e})")

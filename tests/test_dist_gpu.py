@@ -14,7 +14,7 @@ import pytest
 from fftconv_amd import shard
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-WORLD, C, B, L, NB = 2, 5, 256, 12000, 80
+C, B, L, NB = 5, 256, 12000, 80
 
 
 def _free_port():
@@ -26,8 +26,10 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["per-channel", "shared"])
-def test_two_ranks_bitwise_equal_one_process(amd, tmp_path, mode):
+@pytest.mark.parametrize("mode,WORLD", [("per-channel", 2), ("shared", 2), ("per-channel", 8)])
+def test_ranks_bitwise_equal_one_process(amd, tmp_path, mode, WORLD):
+    """WORLD 8: the cfg4 shape (8 ranks, contiguous channel shards) rehearsed
+    with 8 rank processes on device 0."""
     out = str(tmp_path / "y.npy")
     port = _free_port()
     procs = []

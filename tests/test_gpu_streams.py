@@ -103,3 +103,33 @@ def test_calls_on_different_caller_streams_stay_ordered(amd, oracle_mod):
         e.append(r.process(x[c, 2 * K * B:3 * K * B]))
         e.append(r.process(x[c, 3 * K * B:]))
         assert_close(y[c], np.concatenate(e), what=f"channel {c}")
+
+
+@pytest.mark.parametrize("kind", ["uniform", "crossfade"])
+def test_update_through_a_capped_stage(amd, kind):
+    """fftconv_set_host_stage_limit (the pinned reservation may be
+    capped or refused): a stage of 3 response rows streams an 8-channel update
+    in chunks -- the outputs are bit-identical to an uncapped handle's, through
+    immediate and (crossfade) pending swaps."""
+    rng = np.random.default_rng(503)
+    C, B, L, NB = 8, 128, 45 * 128, 48
+    irs = [np.stack([ir(rng, L) for _ in range(C)]) for _ in range(4)]
+    x = white(rng, C * NB * B).reshape(C, NB * B)
+    outs = []
+    for cap in (0, 3 * L * 4):
+        amd.set_host_stage_limit(cap)
+        try:
+            if kind == "uniform":
+                conv = amd.FFTConvolver.init(irs[0], B, L, channels=C)
+            else:
+                conv = amd.CrossfadeConvolver.init(irs[0], B, L, channels=C)
+        finally:
+            amd.set_host_stage_limit(0)
+        assert amd.get_host_stage_limit() == 0
+        y = []
+        for j in range(NB):
+            if j in (5, 9, 30):  # (crossfade: the 9 lands while the fade from 5 runs -> pending)
+                conv.update(irs[1 + [5, 9, 30].index(j)])
+            y.append(conv.process(x[:, j * B:(j + 1) * B]))
+        outs.append(np.concatenate(y, axis=1))
+    assert np.array_equal(outs[0], outs[1])
