@@ -247,6 +247,11 @@ struct UniformCore {
     DevPtr<float> overlap, inbuf, staging;
     DevPtr<int4> state;
     hipStream_t stream = nullptr;
+    // an inner convolver (of a two-stage or a crossfade) runs on its owner's
+    // stream: `parent_stream`, set before init / clone_from, is borrowed
+    // instead of created, so a composite handle holds 2 HIP streams, not 5
+    // (fewer streams sharing the process's hardware queues)
+    hipStream_t parent_stream = nullptr;
     Scratch scratch;
     // host IR uploads (update_host), [C][ir_len]: only a standalone batch
     // owns one (own_stage, set before init).  A crossfade's a / b stage
@@ -273,7 +278,7 @@ struct UniformCore {
             DeviceGuard g(device);
             (void)order.drain(stream);  // (work still queued on a caller stream reads these buffers)
             if (trace_slots) dump_trace();
-            (void)hipStreamDestroy(stream);
+            if (!parent_stream) (void)hipStreamDestroy(stream);
         }
     }
 
@@ -306,7 +311,8 @@ struct UniformCore {
         S = ceil_div(ir_len, B);                                   // :117
         if (S * B > (size_t)INT32_MAX || C > (size_t)INT32_MAX)
             return fail(FFTCONV_E_UNSUPPORTED, "geometry exceeds 32-bit indexing");
-        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        if (parent_stream) stream = parent_stream;
+        else HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         if (int r = H.alloc(C * S * B)) return r;
         if (int r = X.alloc(C * S * B)) return r;
         if (int r = pre.alloc(C * B)) return r;
@@ -572,7 +578,8 @@ struct UniformCore {
         if (int r = o.order.drain(o.stream)) return r;
         device = o.device;
         C = o.C; ir_len = o.ir_len; B = o.B; log2b = o.log2b; S = o.S;
-        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        if (parent_stream) stream = parent_stream;
+        else HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         auto cp = [&](auto &dst, const auto &src) -> int {
             if (int r = dst.alloc(src.n)) return r;
             if (src.n) HIP_TRY(hipMemcpyAsync(dst.p, src.p, src.bytes(), hipMemcpyDeviceToDevice, stream));
@@ -669,7 +676,9 @@ struct TwoStageCore {
     ~TwoStageCore() {
         DeviceGuard g(device);
         if (side) { (void)hipStreamSynchronize(side); (void)hipStreamDestroy(side); }
-        if (stream) { (void)order.drain(stream); (void)hipStreamDestroy(stream); }
+        if (stream) (void)order.drain(stream);
+        head.reset(); tail0.reset(); tail.reset();  // (they borrow `stream`)
+        if (stream) (void)hipStreamDestroy(stream);
         if (ev_main) (void)hipEventDestroy(ev_main);
         if (ev_tail) (void)hipEventDestroy(ev_tail);
     }
@@ -789,12 +798,14 @@ struct TwoStageCore {
         const size_t head_ir_len = std::min(max_len, T);                        // :352-354
         head.reset(new (std::nothrow) UniformCore());
         if (!head) return fail(FFTCONV_E_NOMEM, "out of host memory");
+        head->parent_stream = stream;
         size_t st = slice(0, head_ir_len, tmp);
         if (int r = head->init(dev, C, tmp.data(), head_ir_len, st, head_bs, head_ir_len)) return r;
         if (max_len > T) {                                                      // :356-368
             const size_t tl = std::min(max_len - T, T);
             tail0.reset(new (std::nothrow) UniformCore());
             if (!tail0) return fail(FFTCONV_E_NOMEM, "out of host memory");
+            tail0->parent_stream = stream;
             st = slice(T, tl, tmp);
             if (int r = tail0->init(dev, C, tmp.data(), tl, st, head_bs, tl)) return r;
         }
@@ -802,6 +813,7 @@ struct TwoStageCore {
             const size_t tl = max_len - 2 * T;
             tail.reset(new (std::nothrow) UniformCore());
             if (!tail) return fail(FFTCONV_E_NOMEM, "out of host memory");
+            tail->parent_stream = stream;
             st = slice(2 * T, tl, tmp);
             if (int r = tail->init(dev, C, tmp.data(), tl, st, T, tl)) return r;
         }
@@ -939,6 +951,7 @@ struct TwoStageCore {
             if (!src) return FFTCONV_OK;
             dst.reset(new (std::nothrow) UniformCore());
             if (!dst) return fail(FFTCONV_E_NOMEM, "out of host memory");
+            dst->parent_stream = stream;
             return dst->clone_from(*src);
         };
         if (int r = cl(head, o.head)) return r;
@@ -1059,6 +1072,7 @@ struct CrossfadeCore {
         if (stream) {
             DeviceGuard g(device);
             (void)order.drain(stream);
+            a.reset(); b.reset();  // (they borrow `stream`)
             (void)hipStreamDestroy(stream);
         }
     }
@@ -1072,6 +1086,7 @@ struct CrossfadeCore {
         a.reset(new (std::nothrow) UniformCore());
         b.reset(new (std::nothrow) UniformCore());
         if (!a || !b) return fail(FFTCONV_E_NOMEM, "out of host memory");
+        a->parent_stream = b->parent_stream = stream;
         if (int r = a->clone_from(conv, false)) return r;  // (update() stages through hstage below)
         if (int r = b->clone_from(conv, false)) return r;
         // A and B start as copies: equal FDLs (FLAG_XSYNC), and one
@@ -1358,6 +1373,7 @@ struct CrossfadeCore {
         a.reset(new (std::nothrow) UniformCore());
         b.reset(new (std::nothrow) UniformCore());
         if (!a || !b) return fail(FFTCONV_E_NOMEM, "out of host memory");
+        a->parent_stream = b->parent_stream = stream;
         if (int r = a->clone_from(*o.a)) return r;
         if (int r = b->clone_from(*o.b)) return r;
         if (int r = buf_a.alloc(o.buf_a.n)) return r;
