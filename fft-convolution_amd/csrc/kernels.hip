@@ -922,15 +922,33 @@ __device__ __forceinline__ float mix_select(float va, float vb, float sel) {
     return sel == MIX_SEL_A ? va : (sel == MIX_SEL_B ? vb : mix_apply(va, vb, sel));
 }
 
-// the mix_value walk of one call (n + 1 entries), one thread, bit-identical
-// to the reference's per-sample `mix_value += step` (:259)
-__device__ __forceinline__ void mix_walk(const CrossfadeMixArgs &a, float *vtab) {
-    float v = a.mix_value0;
+// The mix_value walk of one call into LDS: vtab[k] = v0 + step + ... + step
+// (k sequential f32 additions, n + 1 entries), one thread, bit-identical to
+// the reference's per-sample `mix_value += step` (:259).  The additions are a
+// dependent chain on one lane; unrolled by 8 with the stores batched after
+// them, the loop is little more than that chain (the rolled loop -- an
+// address, a store and the loop test per add -- took ~9 us for 512 samples in
+// the cfg5 step workgroups, more than their whole transform chain, r3).
+__device__ __forceinline__ void mix_walk_lane(float *vtab, float v, float step, int n) {
     vtab[0] = v;
-    for (int k = 1; k <= a.n; ++k) {
-        v = __fadd_rn(v, a.step);
+    int k = 1;
+    for (; k + 7 <= n; k += 8) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            v = __fadd_rn(v, step);
+            t[u] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vtab[k + u] = t[u];
+    }
+    for (; k <= n; ++k) {
+        v = __fadd_rn(v, step);
         vtab[k] = v;
     }
+}
+__device__ __forceinline__ void mix_walk(const CrossfadeMixArgs &a, float *vtab) {
+    mix_walk_lane(vtab, a.mix_value0, a.step, a.n);
 }
 
 #include "la.hpp"  // (after the mix helpers: B's lookahead launch can fuse the mix)

@@ -750,16 +750,8 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     if (wave >= NCH) {
         if constexpr (XF == 3) {
             if (wave == NCH) {  // this call's mix_value walk (:259), one lane, then arrive
-                if (a.mix.approaching && lane == 0) {
-                    const int n = a.mix.n;
-                    const float step = a.mix.step;
-                    float v = a.mix.mix_value0;
-                    vtab[0] = v;
-                    for (int q = 1; q <= n; ++q) {  // one f32 rounding each, as the reference
-                        v = __fadd_rn(v, step);
-                        vtab[q] = v;
-                    }
-                }
+                if (a.mix.approaching && lane == 0)  // one f32 rounding each, as the reference
+                    mix_walk_lane(vtab, a.mix.mix_value0, a.mix.step, a.mix.n);
                 la_xf_arrive(a, xcnt, yA, yB, vtab, (size_t)CS(0));
             }
         }
@@ -988,14 +980,7 @@ __device__ __attribute__((noinline)) void la_fallback_xf(const ProcArgs *ap, int
     }
     float *t = reinterpret_cast<float *>(smem);
     if (m.approaching) {
-        if (threadIdx.x == 0) {
-            float v = m.mix_value0;
-            t[0] = v;
-            for (int q = 1; q <= m.n; ++q) {
-                v = __fadd_rn(v, m.step);
-                t[q] = v;
-            }
-        }
+        if (threadIdx.x == 0) mix_walk_lane(t, m.mix_value0, m.step, m.n);
         __syncthreads();
     }
     const float *ya = m.buf_a + (size_t)c * m.buf_stride, *yb = m.buf_b + (size_t)c * m.buf_stride;
@@ -1018,14 +1003,7 @@ __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsign
     float *mt = ap->mix_tab;
     float *t = reinterpret_cast<float *>(smem);
     if (m.approaching) {
-        if (threadIdx.x == 0) {
-            float v = m.mix_value0;
-            t[0] = v;
-            for (int k = 1; k <= m.n; ++k) {  // mix_value += step (:259), one f32 rounding each
-                v = __fadd_rn(v, m.step);
-                t[k] = v;
-            }
-        }
+        if (threadIdx.x == 0) mix_walk_lane(t, m.mix_value0, m.step, m.n);  // mix_value += step (:259)
         __syncthreads();
     }
     for (int j = threadIdx.x; j < m.n; j += LA_NT) mt[j] = mix_selector(m, j, t);
