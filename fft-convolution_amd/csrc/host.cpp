@@ -233,6 +233,8 @@ struct PinnedStage {
     }
 };
 
+int lg_tables(int dev, int log2m, LgTab *out);
+
 // ---------------------------------------------------------------------------
 // UniformCore -- a batch of FFTConvolver instances
 // ---------------------------------------------------------------------------
@@ -272,6 +274,16 @@ struct UniformCore {
     std::vector<long long> trace_meta;  // per slot: la_t, grid
     int la_seq = 1;               // launch tag, alternating 1 / 2
     bool la_all = true;           // next lookahead launch re-anchors every channel
+    // long-block path (B > 2^kMaxLog2Fused, large.hip): per-call progress,
+    // the inverse's scratch, the geometry's tables; lg_whole: every call
+    // since init / reset was whole blocks, so every channel's buffer is empty
+    // at a call's start (a failed C2R freezes fill at 0 then) and a call of
+    // m blocks is exactly m chunks -- else one more chunk bounds any channel
+    bool large = false;
+    DevPtr<int4> lg_prog;
+    DevPtr<float2> lg_v;
+    LgTab lgt{};
+    bool lg_whole = true;
 
     ~UniformCore() {
         if (stream) {
@@ -307,7 +319,8 @@ struct UniformCore {
         B = next_pow2(max_block_size);                             // :115
         log2b = ilog2(B);
         if (log2b > kMaxLog2Block)
-            return fail(FFTCONV_E_UNSUPPORTED, "block size " + std::to_string(B) + " exceeds 8192");
+            return fail(FFTCONV_E_UNSUPPORTED, "block size " + std::to_string(B) + " exceeds 2^22");
+        large = log2b > kMaxLog2Fused;
         S = ceil_div(ir_len, B);                                   // :117
         if (S * B > (size_t)INT32_MAX || C > (size_t)INT32_MAX)
             return fail(FFTCONV_E_UNSUPPORTED, "geometry exceeds 32-bit indexing");
@@ -323,6 +336,8 @@ struct UniformCore {
         if (int r = staging.alloc(C * ir_len)) return r;  // update() never allocates
         if (own_stage)
             if (int r = hstage.alloc(C * ir_len, ir_len)) return r;
+        if (large)
+            if (int r = alloc_large()) return r;
         la_W = la_ok ? la_parts(log2b, (int)S) : 0;
         if (la_W) {
             const LaDims d = la_dims(log2b, (int)S);
@@ -351,6 +366,23 @@ struct UniformCore {
         return FFTCONV_OK;
     }
 
+    // long-block path buffers (B > 2^kMaxLog2Fused); the tables are shared
+    // per (device, geometry); W_N^k is the handle's own `tw`
+    int alloc_large() {
+        if (int r = lg_prog.alloc(C)) return r;
+        if (C) HIP_TRY(hipMemset(lg_prog.p, 0, lg_prog.bytes()));
+        if (int r = lg_v.alloc(C * B)) return r;
+        if (int r = lg_tables(device, log2b, &lgt)) return r;
+        lgt.twN = tw.p;
+        lg_whole = true;
+        return FFTCONV_OK;
+    }
+    // chunks of an n-sample call, an upper bound over the channels
+    int lg_chunks(size_t n) const {
+        return (int)(lg_whole && n % B == 0 ? n / B : (n + B - 1) / B + 1);
+    }
+    void lg_note_call(size_t n) { lg_whole = lg_whole && n % B == 0; }
+
     // fresh state: zero FDL/overlap/buffers, {current 0, active S, fill 0}
     int zero_state() {
         if (X.n) HIP_TRY(hipMemsetAsync(X.p, 0, X.bytes(), stream));
@@ -371,6 +403,10 @@ struct UniformCore {
         a.src = src; a.src_stride = (long long)stride;
         a.len_data = (long long)len_data; a.len_active = (long long)len_active;
         a.tw = tw.p; a.S = (int)S; a.chan0 = (int)chan0; a.update_state = update_state ? 1 : 0;
+        if (large) {
+            HIP_TRY(launch_ir_large(log2b, a, lgt, (int)nch, s));
+            return FFTCONV_OK;
+        }
         HIP_TRY(launch_ir_segments(log2b, a, (int)nch, s));
         // the updated channels dropped their windows: rebuild them now, in
         // the update, so the next process launch stays a steady-state one
@@ -467,6 +503,7 @@ struct UniformCore {
         if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), s));
         if (pre.n) HIP_TRY(hipMemsetAsync(pre.p, 0, pre.bytes(), s));
         HIP_TRY(launch_reset_state(state.p, (int)C, s));
+        lg_whole = true;
         if (la_W && !la_full_variant()) {  // windows of the zeroed FDL, in the reset
             la_all = false;
             return la_rebuild(s, 0, C);
@@ -480,7 +517,16 @@ struct UniformCore {
         j.H = H.p; j.X = X.p; j.overlap = overlap.p; j.inbuf = inbuf.p; j.pre = pre.p; j.state = state.p;
         j.in = din; j.in_stride = (long long)is; j.out = dout; j.out_stride = (long long)os;
         j.S = (int)S; j.n = (int)n;
+        j.lg_prog = lg_prog.p; j.lg_v = lg_v.p;
         return j;
+    }
+    // the long-block fields of a launch of this batch's n-sample call (the
+    // call is counted: a launch failure after this leaves lg_whole pessimistic)
+    void lg_fill(ProcArgs &a, size_t n) {
+        if (!large) return;
+        a.lg = lgt;
+        a.lg_chunks = std::max(a.lg_chunks, lg_chunks(n));
+        lg_note_call(n);
     }
 
     // a call of whole blocks takes the lookahead launch, one
@@ -554,6 +600,7 @@ struct UniformCore {
             if (int r = trace_fill(a, s)) return r;
             ++la_t;
         }
+        lg_fill(a, n);
         HIP_TRY(launch_process(log2b, a, (int)C, s));
         return FFTCONV_OK;
     }
@@ -594,6 +641,11 @@ struct UniformCore {
         if (int r = cp(state, o.state)) return r;
         if (int r = cp(laW, o.laW)) return r;
         la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
+        large = o.large;
+        if (large) {  // (the progress words are zero between calls)
+            if (int r = alloc_large()) return r;
+            lg_whole = o.lg_whole;
+        }
         if (o.trace_slots) {  // (tuning: a clone keeps its own timeline)
             trace_slots = o.trace_slots;
             trace_grid = o.trace_grid;
@@ -620,8 +672,9 @@ struct UniformCore {
         out[0] = row[0].x;
         out[1] = 0.f;
         for (size_t k = 1; k < B; ++k) {
-            out[2 * k] = row[k].x;
-            out[2 * k + 1] = row[k].y;
+            const size_t p = large ? lg_position(log2b, k) : k;  // (long blocks: transposed bin order)
+            out[2 * k] = row[p].x;
+            out[2 * k + 1] = row[p].y;
         }
         out[2 * B] = row[0].y;
         out[2 * B + 1] = 0.f;
@@ -776,7 +829,7 @@ struct TwoStageCore {
                         "max_response_length must be at least the length of the initial impulse response");
         if (int r = check_device(dev)) return r;
         if (ilog2(T) > kMaxLog2Block)
-            return fail(FFTCONV_E_UNSUPPORTED, "tail block size " + std::to_string(T) + " exceeds 8192");
+            return fail(FFTCONV_E_UNSUPPORTED, "tail block size " + std::to_string(T) + " exceeds 2^22");
         device = dev;
         C = channels;
         DeviceGuard g(dev);
@@ -848,7 +901,8 @@ struct TwoStageCore {
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t len, hipStream_t s) {
         if (len > head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
         if (len == 0 || C == 0) return FFTCONV_OK;
-        if (len == head_bs && tail_input_fill % head_bs == 0 && tail_input_fill + len <= T) {
+        if (len == head_bs && tail_input_fill % head_bs == 0 && tail_input_fill + len <= T &&
+            head->log2b <= kMaxLog2Fused) {
             // aligned call: one sub-chunk, and tail0 consumes exactly this block.
             // One launch: head (+ the sub-chunk epilogue) and tail0 as two jobs.
             ProcArgs a{};
@@ -1305,7 +1359,7 @@ struct CrossfadeCore {
                 poisoned = true;
                 return r;
             }
-            HIP_TRY(launch_crossfade_mix(mix_args(dout, os, out_len), (int)C, s));
+            if (int r = launch_mix(dout, os, out_len, s)) return r;
             xf.advance(out_len);
             return FFTCONV_OK;
         }
@@ -1327,10 +1381,24 @@ struct CrossfadeCore {
                 xf.advance(out_len);
                 return FFTCONV_OK;
             }
+            a->lg_fill(pa, m);
+            b->lg_fill(pa, m);
             HIP_TRY(launch_process(a->log2b, pa, (int)C, s));
         }
-        HIP_TRY(launch_crossfade_mix(mix_args(dout, os, out_len), (int)C, s));  // :75-77
+        if (int r = launch_mix(dout, os, out_len, s)) return r;  // :75-77
         xf.advance(out_len);
+        return FFTCONV_OK;
+    }
+
+    // the stand-alone mix (:75-77); a call longer than the mix kernel's LDS
+    // walk first walks mix_value once into mix_tab
+    int launch_mix(float *dout, size_t os, size_t out_len, hipStream_t s) {
+        CrossfadeMixArgs x = mix_args(dout, os, out_len);
+        if (out_len > 1024 && x.approaching) {
+            HIP_TRY(launch_crossfade_walk(x, mix_tab.p, s));
+            x.vtab = mix_tab.p;
+        }
+        HIP_TRY(launch_crossfade_mix(x, (int)C, s));
         return FFTCONV_OK;
     }
 
@@ -1421,12 +1489,53 @@ int fft_twiddles(int dev, int log2n, hipStream_t s, const float2 **out) {
     return FFTCONV_OK;
 }
 
+// The long-block path's tables for M = 2^log2m (lg_split: M = M1 x M2), one
+// set per (device, M), built in f64 and rounded to f32 like every other
+// table: W_M^j (j < M), W_{2 M1}^i (i < 2 M1), W_{2 M2}^i (i < 2 M2).  The
+// caller sets twN (its W_N table).  Synchronous upload on first use.
+int lg_tables(int dev, int log2m, LgTab *out) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, float2 *> tabs;
+    std::lock_guard<std::mutex> lk(mu);
+    int l1 = 0, l2 = 0;
+    lg_split(log2m, &l1, &l2);
+    const size_t M = (size_t)1 << log2m, A = (size_t)2 << l1, Bt = (size_t)2 << l2;
+    auto it = tabs.find({dev, log2m});
+    float2 *p = nullptr;
+    if (it != tabs.end()) {
+        p = it->second;
+    } else {
+        std::vector<float2> t(M + A + Bt);
+        auto fill = [&](float2 *dst, size_t n, size_t period) {
+            for (size_t k = 0; k < n; ++k) {
+                const double ang = -2.0 * M_PI * (double)k / (double)period;
+                dst[k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+            }
+        };
+        fill(t.data(), M, M);
+        fill(t.data() + M, A, A);
+        fill(t.data() + M + A, Bt, Bt);
+        HIP_TRY(hipMalloc((void **)&p, t.size() * sizeof(float2)));
+        hipError_t e = hipMemcpy(p, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            return fail(FFTCONV_E_DEVICE, std::string("twiddle upload: ") + hipGetErrorString(e));
+        }
+        tabs[{dev, log2m}] = p;
+    }
+    out->twN = nullptr;
+    out->twM = p;
+    out->twA = p + M;
+    out->twB = p + M + A;
+    return FFTCONV_OK;
+}
+
 // Fft::forward / inverse on device rows (src/fft_convolver.rs:36-49)
 int fft_rows(int device, size_t n, size_t rows, const float *din, size_t is, float *dout, size_t os, int *status,
              bool inverse, hipStream_t s) {
     if (int r = check_device(device)) return r;
     if (n < 2 || (n & (n - 1)) || n > ((size_t)2 << kMaxLog2Block))
-        return fail(FFTCONV_E_UNSUPPORTED, "Fft length must be a power of two in 2..16384 (N = 2 * block)");
+        return fail(FFTCONV_E_UNSUPPORTED, "Fft length must be a power of two in 2..2^23 (N = 2 * block)");
     const size_t cin = inverse ? n + 2 : n, cout = inverse ? n : n + 2;
     if (rows > (size_t)INT32_MAX || (rows > 1 && (is < cin || os < cout)))
         return fail(FFTCONV_E_INVALID, "row strides shorter than a row");
@@ -1436,7 +1545,23 @@ int fft_rows(int device, size_t n, size_t rows, const float *din, size_t is, flo
     if (int r = fft_twiddles(device, ilog2(n), s, &tw)) return r;
     FftArgs a{};
     a.in = din; a.in_stride = (long long)is; a.out = dout; a.out_stride = (long long)os; a.tw = tw; a.status = status;
-    HIP_TRY(launch_fft_rows(ilog2(n) - 1, inverse, a, (int)rows, s));
+    const int log2m = ilog2(n) - 1;
+    if (log2m > kMaxLog2Fused) {
+        // the long-block passes (large.hip) through a stream-ordered scratch
+        // of up to 64 MiB of rows (the public Fft is not the real-time path)
+        LgTab t{};
+        if (int r = lg_tables(device, log2m, &t)) return r;
+        t.twN = tw;
+        const size_t m = n / 2;
+        const size_t batch = std::max<size_t>(1, std::min(rows, ((size_t)64 << 20) / (m * sizeof(float2))));
+        float2 *scr = nullptr;
+        HIP_TRY(hipMallocAsync((void **)&scr, batch * m * sizeof(float2), s));
+        const hipError_t e = launch_fft_large(log2m, inverse, a, t, scr, (int)rows, (int)batch, s);
+        HIP_TRY(hipFreeAsync(scr, s));
+        HIP_TRY(e);
+        return FFTCONV_OK;
+    }
+    HIP_TRY(launch_fft_rows(log2m, inverse, a, (int)rows, s));
     return FFTCONV_OK;
 }
 

@@ -114,6 +114,28 @@ __device__ __forceinline__ int la_clear(int flags, const ProcArgs &a) {
 }
 __device__ __forceinline__ bool slot0_finite(float4 v) { return isfinite(v.x) && isfinite(v.y); }
 __device__ __forceinline__ bool slot0_finite(float2 v) { return isfinite(v.x) && isfinite(v.y); }
+__device__ __forceinline__ float2 slot0_of(float4 v) { return make_float2(v.x, v.y); }
+__device__ __forceinline__ float2 slot0_of(float2 v) { return v; }
+
+// realfft's C2R error (:264-267) once conv's slot 0 = pre0 + x0 (.) h0 came
+// out non-finite.  The reference's DC / Nyquist imaginary parts are sums of
+// re * 0 + 0 * re products (complex_multiply_accumulate on real bins): NaN
+// exactly when one operand row's (DC, Nyquist) pair is not finite, and 0 when
+// all are finite -- a finite overflow then runs the C2R on inf without an
+// error.  pre0 was summed from rows 1..act-1 of H and of the ring, which are
+// unchanged since (an update zeroes pre_multiplied), so only a non-finite pre0
+// needs them scanned.  Rare path: one lane.
+__device__ __attribute__((noinline)) bool c2r_rejects(const float2 *Hc, const float2 *Xc, int B, int cur, int act,
+                                                      float2 pre0, float2 x0, float2 h0) {
+    if (!slot0_finite(x0) || !slot0_finite(h0)) return true;
+    if (slot0_finite(pre0)) return false;
+    int xi = cur;
+    for (int i = 1; i < act; ++i) {
+        if (++xi == act) xi = 0;
+        if (!slot0_finite(Hc[(size_t)i * B]) || !slot0_finite(Xc[(size_t)xi * B])) return true;
+    }
+    return false;
+}
 
 // Buffer-resource streams (guide T8): one wave-uniform descriptor per channel
 // stream, the row offset in an SGPR (soffset) when the row is wave-uniform,
@@ -487,7 +509,10 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
                                        reinterpret_cast<const float4 *>(h0l)[f], f);
             reinterpret_cast<float4 *>(Z)[f] = cv;
-            if (f == 0 && !slot0_finite(cv)) bad = true;
+            if (f == 0 && !slot0_finite(cv) &&
+                c2r_rejects(Hc, Xc, B, cur, act, slot0_of(reinterpret_cast<const float4 *>(prel)[0]),
+                            slot0_of(reinterpret_cast<const float4 *>(Q)[0]), slot0_of(reinterpret_cast<const float4 *>(h0l)[0])))
+                bad = true;
         }
         // row 1 of the next block's pre_multiplied: H[1] (.) X_new (X_new is row (curp+1) % act = cur)
         if (act > 1 && rsub == 0) {
@@ -786,9 +811,12 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
                 const int f = f0 + s * NT;
                 const vec_t cv = slot_mac(pacc[s], q[f], reinterpret_cast<const vec_t *>(h0g)[f], f);
                 zc[f] = cv;
-                // realfft's C2R rejects a non-zero DC/Nyquist imaginary part,
-                // which only a non-finite operand can produce (:264-267)
-                if (f == 0 && !slot0_finite(cv)) s_err = 1;
+                // realfft's C2R rejects a non-zero DC/Nyquist imaginary part
+                // (:264-267), which only a non-finite operand produces
+                if (f == 0 && !slot0_finite(cv) &&
+                    c2r_rejects(Hc, Xc, B, cur, act, slot0_of(pacc[s]), slot0_of(q[f]),
+                                slot0_of(reinterpret_cast<const vec_t *>(h0g)[f])))
+                    s_err = 1;
             }
         }
         __syncthreads();
@@ -964,7 +992,14 @@ __global__ void crossfade_mix_kernel(CrossfadeMixArgs a) {
         if (threadIdx.x == 0) mix_walk(a, vtab);
         __syncthreads();
     }
-    for (int j = threadIdx.x; j < a.n; j += blockDim.x) o[j] = mix_sample(a, j, A[j], Bv[j], tab ? vtab : nullptr);
+    const float *vt = tab ? vtab : (a.approaching ? a.vtab : nullptr);
+    for (int j = threadIdx.x; j < a.n; j += blockDim.x) o[j] = mix_sample(a, j, A[j], Bv[j], vt);
+}
+
+// the mix_value walk of a call longer than crossfade_mix_kernel's LDS table
+// (n > 1024) into a device table, once (one lane), before the mix reads it
+__global__ void crossfade_walk_kernel(CrossfadeMixArgs a, float *vtab) {
+    if (threadIdx.x == 0) mix_walk(a, vtab);
 }
 
 // ---------------------------------------------------------------------------
@@ -1083,7 +1118,11 @@ __device__ __forceinline__ void pair_step(const ProcArgs &a, size_t c, int cur, 
                 const vec_t cv = slot_mac(pacc[j][s], reinterpret_cast<const vec_t *>(bufC)[f],
                                           reinterpret_cast<const vec_t *>(h0[j])[f], f);
                 reinterpret_cast<vec_t *>(Z)[f] = cv;
-                if (f == 0 && !slot0_finite(cv)) s_err[j] = 1;
+                if (f == 0 && !slot0_finite(cv) &&
+                    c2r_rejects(J.H + c * rows, Js[0]->X + c * rows, B, cur, act, slot0_of(pacc[j][s]),
+                                slot0_of(reinterpret_cast<const vec_t *>(bufC)[f]),
+                                slot0_of(reinterpret_cast<const vec_t *>(h0[j])[f])))
+                    s_err[j] = 1;
             }
         }
         __syncthreads();
@@ -1800,13 +1839,6 @@ static hipError_t launch_ir_t(const IrArgs &a, int channels, hipStream_t s) {
     return hipGetLastError();
 }
 
-#ifdef FFTCONV_DEBUG_BOUNDS  // (debug builds: block 256 only, to keep the compile short)
-#define FFTCONV_DISPATCH(FN, LOG2B, ...)                      \
-    switch (LOG2B) {                                          \
-        case 8: return FN<8>(__VA_ARGS__);                    \
-        default: return hipErrorNotSupported;                 \
-    }
-#else
 #define FFTCONV_DISPATCH(FN, LOG2B, ...)                      \
     switch (LOG2B) {                                          \
         case 0: return FN<0>(__VA_ARGS__);                    \
@@ -1825,10 +1857,10 @@ static hipError_t launch_ir_t(const IrArgs &a, int channels, hipStream_t s) {
         case 13: return FN<13>(__VA_ARGS__);                  \
         default: return hipErrorInvalidValue;                 \
     }
-#endif
 
 hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;
+    if (log2b > kMaxLog2Fused) return launch_process_large(log2b, a, a.lg, a.lg_chunks, channels, s);
     FFTCONV_DISPATCH(launch_process_t, log2b, a, channels, s)
 }
 
@@ -2016,6 +2048,12 @@ hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipSt
 hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStream_t s) {
     if (channels <= 0 || a.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(crossfade_mix_kernel, dim3(channels), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_crossfade_walk(const CrossfadeMixArgs &a, float *vtab, hipStream_t s) {
+    if (a.n <= 0 || !a.approaching) return hipSuccess;
+    hipLaunchKernelGGL(crossfade_walk_kernel, dim3(1), dim3(64), 0, s, a, vtab);
     return hipGetLastError();
 }
 

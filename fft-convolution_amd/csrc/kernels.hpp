@@ -75,6 +75,19 @@ struct ProcJob {
     // block, in / out advanced by mk * B): blocks of the whole call, this
     // launch's block (0 / 0 otherwise)
     int mcall, mk;
+    // long-block path (B > 2^kMaxLog2Fused, large.hip): per channel the
+    // call's progress {processed, done, C2R failed, arrival counter}, and the
+    // [C][B] scratch between the row and the column passes of the inverse
+    int4 *lg_prog;
+    float2 *lg_v;
+};
+
+// Twiddle tables of the long-block path (large.hip), f64-rounded f32:
+// twN = W_N^k (k < N/2, the post/pre-twiddle), twM = W_M^j (j < M = N/2, the
+// four-step's inner twiddle), twA / twB = W_{2 M1}^i / W_{2 M2}^i (the column
+// and row FFTs), M = M1 x M2 (lg_split)
+struct LgTab {
+    const float2 *twN, *twM, *twA, *twB;
 };
 
 // Crossfader::mix over one call's samples (src/crossfade_convolver.rs:242-278),
@@ -92,6 +105,7 @@ struct CrossfadeMixArgs {
     long long fading;
     float mix_value0;
     float step;
+    const float *vtab;     // calls longer than 1024 samples: the mix_value walk (launch_crossfade_walk), or null
 };
 
 // Up to two jobs of the same block size in one launch (grid.y = job): the
@@ -129,6 +143,10 @@ struct ProcArgs {
     // << 4, HW_ID low 16 bits | XCC_ID << 24, t0, t1} (s_memrealtime, 100 MHz)
     int4 *la_trace;        // this launch's record: [la_trace_grid][4 waves] + phase stamps after it
     int la_trace_grid;
+    // long-block path (launch_process with log2b > kMaxLog2Fused): the
+    // geometry's tables and the chunks to run (an upper bound over channels)
+    LgTab lg;
+    int lg_chunks;
 };
 
 struct IrArgs {
@@ -230,6 +248,24 @@ bool tail0_defer_supported(int log2b, int act, int nmax);
 bool tail0_defer_allowed();  // VARIANT_T0BLOCK unset
 hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s);
 
-constexpr int kMaxLog2Block = 13;  // B <= 8192 (two B-point complex LDS buffers = 128 KiB)
+// The fused one-workgroup-per-channel kernels hold two B-point complex
+// buffers in LDS: B <= 8192 (128 KiB).  Larger blocks, up to 2^22, take the
+// four-step long-block path (large.hip).
+constexpr int kMaxLog2Fused = 13;
+constexpr int kMaxLog2Block = 22;
+// M = 2^log2b = M1 x M2 of the long-block path; bin k of a spectrum row sits
+// at position (k mod M1) * M2 + k / M1
+void lg_split(int log2b, int *l1, int *l2);
+size_t lg_position(int log2b, size_t k);
+hipError_t launch_process_large(int log2b, const ProcArgs &a, const LgTab &t, int chunks, int channels,
+                                hipStream_t s);
+hipError_t launch_ir_large(int log2b, const IrArgs &a, const LgTab &t, int channels, hipStream_t s);
+// the public Fft's rows through the same passes: rows in batches of `batch`,
+// scratch [batch][N/2] complex
+hipError_t launch_fft_large(int log2m, bool inverse, const FftArgs &a, const LgTab &t, float2 *scratch, int rows,
+                            int batch, hipStream_t s);
+// crossfade mix of calls longer than the in-LDS walk (n > 1024): the walk
+// once into a device table (one lane), then the mix reading it
+hipError_t launch_crossfade_walk(const CrossfadeMixArgs &a, float *vtab, hipStream_t s);
 
 }  // namespace fftconv

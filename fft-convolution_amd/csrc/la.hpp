@@ -833,7 +833,10 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
                                    h0r[i], f);
         reinterpret_cast<float4 *>(Z)[f] = cv;
-        if (f == 0 && !slot0_finite(cv)) bad = true;
+        if (f == 0 && !slot0_finite(cv) &&
+            c2r_rejects(JC.H + c * rows, XK(k) + c * rows, B, cur, act, slot0_of(reinterpret_cast<const float4 *>(prel)[0]),
+                        slot0_of(reinterpret_cast<const float4 *>(Q)[0]), slot0_of(h0r[0])))
+            bad = true;
     }
     const bool err = __ballot(bad) != 0ull;
     wave_sync();
@@ -905,11 +908,17 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
     for (int k = 0; k < nvalid; ++k) {
         if (k) __syncthreads();
         const int c = c0 + k;
-        const int4 st = J.state[c];
+        int4 st = J.state[c];
         if (XF == 0 && (st.w & FLAG_CALLDONE)) {
-            // done with this multi-block call; its last launch clears the flag
-            if (J.mk == J.mcall - 1 && threadIdx.x == 0) J.state[c] = make_int4(st.x, st.y, st.z, la_clear(st.w & ~FLAG_CALLDONE, a));
-            continue;
+            if (J.mcall > 1 && J.mk > 0) {
+                // done with this multi-block call; its last launch clears the flag
+                if (J.mk == J.mcall - 1 && threadIdx.x == 0) J.state[c] = make_int4(st.x, st.y, st.z, la_clear(st.w & ~FLAG_CALLDONE, a));
+                continue;
+            }
+            // a stale flag: the call that set it stopped before its last
+            // launch (a failed launch).  This is a new call's first
+            // block: process it (the state written below drops the flag)
+            st.w &= ~FLAG_CALLDONE;
         }
         if (XF == 0 && J.mcall > 1 && J.mk == 0 && !la_eligible<LOG2B>(st, J.n)) {
             // off the lookahead path at the start of a multi-block call

@@ -484,6 +484,10 @@ int ots_process(ots_t *t, const float *input, float *output, size_t len) {
         size_t processing = H - (t->tail_input_fill % H);
         if (remaining < processing) processing = remaining;
         size_t sb = processed, se = processed + processing;
+        /* a head that does not divide T runs past the tail buffers: the
+           reference panics at its first out-of-range index (:442, before the
+           :459-460 slice); check before touching them (ASan, r4) */
+        if (t->precalculated_pos + processing > T || t->tail_input_fill + processing > T) return -1;
         {   /* :439-445 */
             size_t p = t->precalculated_pos;
             for (size_t i = sb; i < se; i++) output[i] += t->tail_precalculated0[p++];
@@ -493,8 +497,6 @@ int ots_process(ots_t *t, const float *input, float *output, size_t len) {
             for (size_t i = sb; i < se; i++) output[i] += t->tail_precalculated[p++];
         }
         t->precalculated_pos += processing;                           /* :456 */
-        /* :459-460 slice panics when head does not divide T (non-power-of-two head) */
-        if (t->tail_input_fill + processing > T) return -1;
         memcpy(t->tail_input + t->tail_input_fill, input + processed, processing * sizeof(float));
         t->tail_input_fill += processing;                             /* :459-461 */
         if (t->tail_input_fill % H == 0) {                            /* :464-476 */

@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# ORACLE_LIB: another build of the same restatement (make asan: liboracle_asan.so)
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 _f32p = C.POINTER(C.c_float)
 _sz = C.c_size_t
