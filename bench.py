@@ -393,6 +393,9 @@ def main():
                 "ir_len": L,
                 "segments": S,
                 "dry_input": args.dry,
+                # --dry shared: one RCCL broadcast per run of ring slots (bucketed), or one per step with --per-call
+                "broadcast": (None if args.dry != "shared" else
+                              ("per-step" if args.per_call else f"bucketed x{args.ring}")),
                 "parallelism": f"channel-shard x{world}",
                 "submission": "per-call" if args.per_call else "process_device_steps",
             },

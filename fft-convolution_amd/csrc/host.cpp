@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -166,7 +167,7 @@ struct StreamOrder {
 // update streams its rows through the stage in chunks, each chunk waiting for
 // the previous one's copy out of it -- still no allocation, but the host
 // waits for all but the last chunk's DMA.
-static size_t g_stage_limit = 0;  // bytes, 0 = none
+static std::atomic<size_t> g_stage_limit{0};  // bytes, 0 = none (set / read from any thread)
 
 struct PinnedStage {
     float *p = nullptr;
@@ -187,7 +188,8 @@ struct PinnedStage {
     int alloc(size_t count, size_t min_count) {
         if (count == 0) return FFTCONV_OK;
         min_count = std::max<size_t>(1, std::min(min_count, count));
-        if (g_stage_limit) count = std::max(min_count, std::min(count, g_stage_limit / sizeof(float)));
+        const size_t lim = g_stage_limit.load(std::memory_order_relaxed);
+        if (lim) count = std::max(min_count, std::min(count, lim / sizeof(float)));
         hipError_t e = hipErrorOutOfMemory;
         for (;;) {
             e = hipHostMalloc((void **)&p, count * sizeof(float), hipHostMallocDefault);
@@ -272,6 +274,8 @@ struct UniformCore {
     DevPtr<int4> trace;
     size_t trace_slots = 0, trace_grid = 0;
     std::vector<long long> trace_meta;  // per slot: la_t, grid
+    hipStream_t probe_side[3] = {};  // FFTCONV_LA_SPLIT timing probe
+    hipEvent_t probe_ev = nullptr;
     int la_seq = 1;               // launch tag, alternating 1 / 2
     bool la_all = true;           // next lookahead launch re-anchors every channel
     // long-block path (B > 2^kMaxLog2Fused, large.hip): per-call progress,
@@ -589,6 +593,26 @@ struct UniformCore {
                     a.la_mix = la_mix;
                     a.mix = *mix;
                     a.mix_tab = mix_tab;
+                }
+                if (la_split_probe() && !la_mix && !la_all) {
+                    // timing probe: the anchors on a side stream after the
+                    // previous steps, the steps not waiting for them
+                    static const int nside = getenv("FFTCONV_LA_SPLIT_SIDES") ? atoi(getenv("FFTCONV_LA_SPLIT_SIDES")) : 1;
+                    if (!probe_side[0]) {
+                        for (int q = 0; q < nside; ++q)
+                            HIP_TRY(hipStreamCreateWithFlags(&probe_side[q], hipStreamNonBlocking));
+                        HIP_TRY(hipEventCreateWithFlags(&probe_ev, hipEventDisableTiming));
+                    }
+                    hipStream_t side = probe_side[la_t % nside];
+                    HIP_TRY(hipEventRecord(probe_ev, s));
+                    HIP_TRY(hipStreamWaitEvent(side, probe_ev, 0));
+                    a.la_part = 1;
+                    HIP_TRY(launch_process_la(log2b, a, (int)C, side));
+                    a.la_part = 2;
+                    HIP_TRY(launch_process_la(log2b, a, (int)C, s));
+                    a.la_part = 0;
+                    la_advance();
+                    continue;
                 }
                 HIP_TRY(launch_process_la(log2b, a, (int)C, s));
                 la_advance();
@@ -1666,10 +1690,10 @@ int fftconv_set_pipeline_lag(int rows) {
 }
 int fftconv_get_pipeline_lag(void) { return get_pipeline_lag(); }
 int fftconv_set_host_stage_limit(size_t bytes) {
-    g_stage_limit = bytes;
+    g_stage_limit.store(bytes, std::memory_order_relaxed);
     return FFTCONV_OK;
 }
-size_t fftconv_get_host_stage_limit(void) { return g_stage_limit; }
+size_t fftconv_get_host_stage_limit(void) { return g_stage_limit.load(std::memory_order_relaxed); }
 
 // ---- uniform --------------------------------------------------------------
 fftconv_uniform *fftconv_uniform_init(const float *response, size_t response_len, size_t max_block_size,

@@ -526,6 +526,11 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     constexpr float invN = 1.0f / (float)(2 * B);
     constexpr size_t chb = LS::ch_bytes;
     static_assert(NCH == 1 || NCH == 2, "one or two channels per step workgroup");
+    // a workgroup barrier after the chains' prologue (XF 3 only: the twiddle
+    // table staged by wave 0 and the mix counter); otherwise the helpers issue
+    // their near and window rows with the launch instead of after the chains'
+    // prologue DMA has landed (r3 timeline: pre at 10.5 us, R2C done at 7.3)
+    constexpr bool TWBAR = NCH > 1 && XF == 3;
     float2 *twl = reinterpret_cast<float2 *>(smem);
     auto chan_lds = [&](int k) { return smem + LS::tw_bytes + (size_t)k * chb; };
     float4 *grp = reinterpret_cast<float4 *>(smem);  // [NCH][GS][F], full pass only
@@ -649,7 +654,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
     float2 *Z = reinterpret_cast<float2 *>(chan_lds(0)), *Q = Z + B;
     if (wave < NCH && wave >= nvalid) {
         // (no channel for this chain wave: it still takes part in the barriers)
-        if constexpr (NCH > 1) __syncthreads();
+        if constexpr (TWBAR) __syncthreads();
     } else if (wave < NCH) {
         // ---- transform chain of channel k = wave: the block -> R2C -> FDL row `current`
         const int k = wave;
@@ -664,7 +669,11 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         const float *inc = JC.in + c * JC.in_stride;
         dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);  // x[0..B) as packed z[0..B/2)
         for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
-        if (k == 0) dma_16b<64>(twl, a.tw, (int)LS::tw_bytes);
+        // the twiddle table: every chain wave stages it (the same bytes), so
+        // no workgroup barrier holds the helpers' first loads behind the
+        // chains' prologue (XF 3: wave 0, then the barrier that also
+        // publishes the mix counter)
+        if (!TWBAR || k == 0) dma_16b<64>(twl, a.tw, (int)LS::tw_bytes);
         if (XF == 3 && k == 0 && lane == 0) *xcnt = 0;  // (visible to all after the barrier below)
 #pragma unroll
         for (int i = 0; i < F / 64; ++i) h0r[i] = reinterpret_cast<const float4 *>(JC.H + c * rows)[lane + 64 * i];
@@ -680,7 +689,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         la_stamp(a, 0);
-        if constexpr (NCH > 1) {
+        if constexpr (TWBAR) {
             __syncthreads();  // wave 0's twiddle table is in LDS
         } else {
             wave_sync();
@@ -699,7 +708,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         wave_r2c_post<LOG2B>(bufA, bufB, twl, Q, JC.X + c * rows + (size_t)cur * B);
         la_stamp(a, 1);
     } else {
-        if constexpr (NCH > 1) __syncthreads();  // (the chain waves' twiddle barrier)
+        if constexpr (TWBAR) __syncthreads();  // (the chain waves' twiddle barrier)
         // ---- pre = near chain (rows D0..1) + (W1 + (W2 + W3)), canonical order
 #pragma unroll
         for (int t = 0; t < TPL; ++t) {
@@ -796,7 +805,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             constexpr int JMS = la_mid_per(LH);
             const int hl = tid - 64 * NCH;
             const int l = __builtin_amdgcn_readfirstlane(hl / F), f = hl % F;
-            if (l * JMS < LA_P1) {
+            if (l * JMS < LA_P1 && a.la_part != 2) {
 #pragma unroll
                 for (int k = 0; k < NCH; ++k) {
                     if (k >= nvalid || !la_sched(CS(k), a, LA_P1)) continue;

@@ -378,7 +378,7 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
             // pre_multiplied = sum_{i=1}^{act-1} H[i] (.) X[(current + i) % act] (:244-255)
 #pragma unroll
             for (int u = 0; u < EP; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            int xi = ch.cur + 1 >= ch.act ? ch.cur + 1 - ch.act : ch.cur + 1;
+            int xi = (ch.cur + 1) % ch.act;  // (current may exceed act after an update shrank it)
             for (int i = 1; i < ch.act; ++i) {
                 const float4 *hr = reinterpret_cast<const float4 *>(Hc + (size_t)i * M);
                 const float4 *xr = reinterpret_cast<const float4 *>(Xc + (size_t)xi * M);
@@ -421,9 +421,8 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
                 // carried pre_multiplied was summed from the same rows.
                 bool bad = !finite2(make_float2(x.x, x.y)) || !finite2(make_float2(h0.x, h0.y));
                 if (!bad && !finite2(make_float2(acc[0].x, acc[0].y))) {
-                    int xi = ch.cur;
                     for (int i = 1; i < ch.act && !bad; ++i) {
-                        if (++xi == ch.act) xi = 0;
+                        const int xi = (ch.cur + i) % ch.act;
                         bad = !finite2(Hc[(size_t)i * M]) || !finite2(Xc[(size_t)xi * M]);
                     }
                 }

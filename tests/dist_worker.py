@@ -18,8 +18,31 @@ from fftconv_amd import shard  # noqa: E402
 def main():
     out_path, mode, C, B, L, NB = sys.argv[1], sys.argv[2], *map(int, sys.argv[3:7])
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     mine = shard.channel_range(rank, world, C)
+    if mode == "shared-nccl":
+        # RCCL (the "nccl" backend on ROCm): the dry blocks broadcast as a
+        # device tensor, then read by every channel with input stride 0
+        dev = torch.device("cuda:0")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        conv = F.FFTConvolver.init(shard.synth_irs(mine, L), B, L, channels=C, device=0)
+        t = (torch.from_numpy(shard.synth_shared_dry(NB, B)).to(dev) if rank == 0
+             else torch.zeros(NB, B, device=dev))
+        shard.broadcast_dry(dist, t, src=0)
+        yd = torch.empty(NB, C, B, device=dev)
+        s = torch.cuda.current_stream(dev)
+        for b in range(NB):
+            conv.process_device(t[b].data_ptr(), 0, yd[b].data_ptr(), B, B, s.cuda_stream)
+        s.synchronize()
+        got = [torch.zeros_like(yd) for _ in range(world)] if rank == 0 else None
+        dist.gather(yd, got, dst=0)
+        if rank == 0:
+            np.save(out_path, torch.cat(got, dim=1).cpu().numpy())
+            with open(out_path + ".backend", "w") as f:
+                f.write(dist.get_backend())
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     conv = F.FFTConvolver.init(shard.synth_irs(mine, L), B, L, channels=C, device=0)
     if mode == "shared":
         t = torch.from_numpy(shard.synth_shared_dry(NB, B)) if rank == 0 else torch.zeros(NB, B)

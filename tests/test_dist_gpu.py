@@ -14,7 +14,9 @@ import pytest
 from fftconv_amd import shard
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-C, B, L, NB = 5, 256, 12000, 80
+# L 17,000 at B 256: S = 67 > 65, so the third anchor level (rows >= 65) is
+# live and its 64-step windows turn over within NB blocks
+C, B, L, NB = 5, 256, 17000, 80
 
 
 def _free_port():
@@ -26,10 +28,14 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,WORLD", [("per-channel", 2), ("shared", 2), ("per-channel", 8)])
+@pytest.mark.parametrize("mode,WORLD", [("per-channel", 2), ("shared", 2), ("per-channel", 8), ("shared-nccl", 1)])
 def test_ranks_bitwise_equal_one_process(amd, tmp_path, mode, WORLD):
     """WORLD 8: the cfg4 shape (8 ranks, contiguous channel shards) rehearsed
-    with 8 rank processes on device 0."""
+    with 8 rank processes on device 0.  shared-nccl: one rank on RCCL (the
+    "nccl" backend; the one-GPU pool cannot host two RCCL ranks on one
+    device) -- init_process_group("nccl") and the dry-block broadcast on a
+    device tensor executed, its output fed to the channels with input stride 0
+    and compared bitwise with the single process."""
     out = str(tmp_path / "y.npy")
     port = _free_port()
     procs = []
@@ -41,10 +47,13 @@ def test_ranks_bitwise_equal_one_process(amd, tmp_path, mode, WORLD):
     rcs = [p.wait(timeout=110) for p in procs]
     assert rcs == [0] * WORLD
     got = np.load(out)  # [NB][WORLD*C][B]
+    if mode == "shared-nccl":
+        with open(out + ".backend") as f:
+            assert f.read() == "nccl"
     full = range(0, WORLD * C)
     conv = amd.FFTConvolver.init(shard.synth_irs(full, L), B, L, channels=WORLD * C, device=0)
     assert conv.lookahead_parts() > 0
-    if mode == "shared":
+    if mode.startswith("shared"):
         dry = np.broadcast_to(shard.synth_shared_dry(NB, B)[:, None, :], (NB, WORLD * C, B))
     else:
         dry = shard.synth_dry(full, NB, B)

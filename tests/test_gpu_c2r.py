@@ -36,6 +36,7 @@ def test_finite_overflow_is_not_a_c2r_error(amd, oracle_mod, B, L, chunks):
     ref = oracle_mod.FFTConvolver.init(h, B, L)
     ncalls = 3 * (L // B + 2)
     seq = [chunks[i % len(chunks)] for i in range(ncalls)]
+    overflowed = False
     for i, k in enumerate(seq):
         if i == 4:
             conv.update(hbig)
@@ -49,8 +50,8 @@ def test_finite_overflow_is_not_a_c2r_error(amd, oracle_mod, B, L, chunks):
         g, r = conv.process(x), ref.process(x)
         _compare(g, r, f"B {B} call {i}")
         assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill), f"call {i}"
-        if i in (5, 6):
-            assert not np.isfinite(r).all()  # the case under test: no error, non-finite output
+        overflowed |= not np.isfinite(r).all()
+    assert overflowed  # the case under test happened: no error, non-finite output
 
 
 def test_finite_overflow_crossfade_pair(amd, oracle_mod):

@@ -464,8 +464,10 @@ def test_uniform_panics(amd):
         conv.update(np.ones(11, np.float32))
     with pytest.raises(amd.ConvolutionPanic):
         conv.process(np.ones(4, np.float32), out_len=8)
+    # block sizes up to 2^22 run (the long-block path, test_gpu_large.py);
+    # past that the build returns FFTCONV_E_UNSUPPORTED
     with pytest.raises(amd.DeviceError):
-        amd.FFTConvolver.init(np.ones(10, np.float32), 16384, 10)
+        amd.FFTConvolver.init(np.ones(10, np.float32), (1 << 22) + 1, 10)
 
 
 @pytest.mark.parametrize("head,L,calls", [(64, 12000, [64]), (32, 5000, [32, 13, 19]), (32, 3000, [1, 31, 32, 16]),
