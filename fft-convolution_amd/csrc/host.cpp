@@ -274,8 +274,6 @@ struct UniformCore {
     DevPtr<int4> trace;
     size_t trace_slots = 0, trace_grid = 0;
     std::vector<long long> trace_meta;  // per slot: la_t, grid
-    hipStream_t probe_side[3] = {};  // FFTCONV_LA_SPLIT timing probe
-    hipEvent_t probe_ev = nullptr;
     int la_seq = 1;               // launch tag, alternating 1 / 2
     bool la_all = true;           // next lookahead launch re-anchors every channel
     // long-block path (B > 2^kMaxLog2Fused, large.hip): per-call progress,
@@ -593,26 +591,6 @@ struct UniformCore {
                     a.la_mix = la_mix;
                     a.mix = *mix;
                     a.mix_tab = mix_tab;
-                }
-                if (la_split_probe() && !la_mix && !la_all) {
-                    // timing probe: the anchors on a side stream after the
-                    // previous steps, the steps not waiting for them
-                    static const int nside = getenv("FFTCONV_LA_SPLIT_SIDES") ? atoi(getenv("FFTCONV_LA_SPLIT_SIDES")) : 1;
-                    if (!probe_side[0]) {
-                        for (int q = 0; q < nside; ++q)
-                            HIP_TRY(hipStreamCreateWithFlags(&probe_side[q], hipStreamNonBlocking));
-                        HIP_TRY(hipEventCreateWithFlags(&probe_ev, hipEventDisableTiming));
-                    }
-                    hipStream_t side = probe_side[la_t % nside];
-                    HIP_TRY(hipEventRecord(probe_ev, s));
-                    HIP_TRY(hipStreamWaitEvent(side, probe_ev, 0));
-                    a.la_part = 1;
-                    HIP_TRY(launch_process_la(log2b, a, (int)C, side));
-                    a.la_part = 2;
-                    HIP_TRY(launch_process_la(log2b, a, (int)C, s));
-                    a.la_part = 0;
-                    la_advance();
-                    continue;
                 }
                 HIP_TRY(launch_process_la(log2b, a, (int)C, s));
                 la_advance();

@@ -1933,8 +1933,8 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         args.la_rebuild = 0;
         args.la_t = a.la_t % LA_PER;
         if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) args.la_all = -1;  // no anchors: every eligible step sums all its rows
-        la_counts(args, LOG2B, a.job[0].S, channels, args.la_all > 0, !LaStep<LOG2B>::MIDIN || a.la_part == 1);
-        if (args.la_all < 0 || a.la_part == 2) args.la_n[0] = args.la_n[1] = args.la_n[2] = 0;
+        la_counts(args, LOG2B, a.job[0].S, channels, args.la_all > 0, !LaStep<LOG2B>::MIDIN);
+        if (args.la_all < 0) args.la_n[0] = args.la_n[1] = args.la_n[2] = 0;
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
@@ -1943,10 +1943,6 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         if (a.la_mix == 2 && a.job[0].add0) return hipErrorInvalidValue;  // (the fused mix uses the add buffers' LDS)
         const int xwg = a.la_mix == 1 ? LA_XWG : 0;  // A's launch: the mix_value walk workgroups
         const int nanch = (xf3 ? 2 : 1) * (args.la_n[0] + args.la_n[1] + args.la_n[2]);
-        if (a.la_part == 1) {
-            if (nanch > 0) hipLaunchKernelGGL(kern, dim3(nanch), dim3(LA_NT), lds, s, args);
-            return hipGetLastError();
-        }
         hipLaunchKernelGGL(kern, dim3(nanch + nstep + xwg), dim3(LA_NT), lds, s, args);
         return hipGetLastError();
     }
@@ -2028,11 +2024,6 @@ static hipError_t launch_rebuild_t(const ProcArgs &a, int channels, hipStream_t 
 hipError_t launch_la_rebuild(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
     if (channels <= 0) return hipSuccess;
     FFTCONV_DISPATCH(launch_rebuild_t, log2b, a, channels, s)
-}
-
-bool la_split_probe() {
-    static const bool on = getenv("FFTCONV_LA_SPLIT") != nullptr;
-    return on;
 }
 
 bool la_full_variant() { return g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL); }

@@ -138,10 +138,6 @@ struct ProcArgs {
     // only, for channels [la_c0, la_channels), as if they had run in the
     // launch before the next one (la_t = that launch's counter)
     int la_rebuild;
-    // timing probe (FFTCONV_LA_SPLIT, results not meaningful): 1 = a launch
-    // of the anchors only (level 1 in workgroups of its own), 2 = the steps
-    // only (no in-step level-1 walk); 0 = the whole launch
-    int la_part;
     int la_c0;
     // launch timeline (tuning only, FFTCONV_LA_TRACE): per wave {role | wave
     // << 4, HW_ID low 16 bits | XCC_ID << 24, t0, t1} (s_memrealtime, 100 MHz)
@@ -225,7 +221,6 @@ LaDims la_dims(int log2b, int S);
 // launch timeline records per lookahead launch (FFTCONV_LA_TRACE): the largest grid
 int la_trace_grid(int log2b, int S, int channels);
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s);
-bool la_split_probe();  // FFTCONV_LA_SPLIT set (timing probe only)
 // every far and mid window of channels [a.la_c0, channels) rebuilt from the
 // current H and FDL (anchors only), then their state words pointed at them
 hipError_t launch_la_rebuild(int log2b, const ProcArgs &a, int channels, hipStream_t s);

@@ -805,7 +805,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
             constexpr int JMS = la_mid_per(LH);
             const int hl = tid - 64 * NCH;
             const int l = __builtin_amdgcn_readfirstlane(hl / F), f = hl % F;
-            if (l * JMS < LA_P1 && a.la_part != 2) {
+            if (l * JMS < LA_P1) {
 #pragma unroll
                 for (int k = 0; k < NCH; ++k) {
                     if (k >= nvalid || !la_sched(CS(k), a, LA_P1)) continue;
