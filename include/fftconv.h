@@ -43,7 +43,7 @@ enum {
     FFTCONV_OK = 0,
     FFTCONV_E_INVALID = -1,       /* a reference panic!/assert!/slice-bounds precondition */
     FFTCONV_E_UNIMPLEMENTED = -2, /* a reference todo!() */
-    FFTCONV_E_UNSUPPORTED = -3,   /* geometry outside this build (block size > 8192) */
+    FFTCONV_E_UNSUPPORTED = -3,   /* geometry outside this build (block size > 2^22) */
     FFTCONV_E_DEVICE = -4,        /* HIP runtime error / no device */
     FFTCONV_E_NOMEM = -5
 };
@@ -63,7 +63,8 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
 /* The reference's public real FFT (realfft's RealToComplex / ComplexToReal of
  * length n) as batched device transforms -- the convolver's own kernels, so a
  * spectrum here is bit-identical to the convolver's.  n: power of two in
- * 2..16384.  Forward (Fft::forward :36-39): rows of n reals -> n/2+1 bins,
+ * 2..2^23 (n > 16384: the four-step passes of the long-block path).
+ * Forward (Fft::forward :36-39): rows of n reals -> n/2+1 bins,
  * interleaved (re, im), unnormalised, DC / Nyquist imaginary parts 0.
  * Inverse (Fft::inverse :41-49): n/2+1 bins -> n reals divided by n;
  * d_status[row] (optional) = 1 where realfft returns FftError::InputValues

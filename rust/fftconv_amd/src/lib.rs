@@ -13,6 +13,8 @@
 pub mod ffi;
 
 use fft_convolution::Convolution;
+use realfft::FftError;
+use rustfft::num_complex::Complex;
 use std::ffi::CStr;
 use std::os::raw::{c_int, c_void};
 use std::ptr::NonNull;
@@ -231,5 +233,44 @@ impl GpuFFTConvolverBatch {
     }
     pub fn channels(&self) -> usize {
         unsafe { ffi::fftconv_uniform_channels(self.h.as_ptr()) }
+    }
+}
+
+/// Fft (src/fft_convolver.rs:7-50): realfft's R2C / C2R of length n on the
+/// GPU -- the convolver's own transforms, so a spectrum here is bit-identical
+/// to the row a handle holds.  n is a power of two in 2..2^23 (the library
+/// returns FFTCONV_E_UNSUPPORTED, and this panics, otherwise).
+#[derive(Clone, Default, Debug)]
+pub struct GpuFft {
+    n: usize,
+    device: i32,
+}
+impl GpuFft {
+    /// Fft::init (:30-34); the device tables are built on first use
+    pub fn init(&mut self, length: usize) {
+        self.n = length;
+    }
+    /// Fft::forward (:36-39): n reals -> n/2 + 1 bins, unnormalised
+    pub fn forward(&self, input: &mut [f32], output: &mut [Complex<f32>]) -> Result<(), FftError> {
+        assert!(input.len() == self.n && output.len() == self.n / 2 + 1, "Fft::forward: slice lengths");
+        check(unsafe {
+            ffi::fftconv_fft_forward_host(self.device, self.n, 1, input.as_ptr(), output.as_mut_ptr() as *mut f32)
+        });
+        Ok(())
+    }
+    /// Fft::inverse (:41-49): n/2 + 1 bins -> n reals / n; a non-zero DC /
+    /// Nyquist imaginary part is realfft's FftError::InputValues, returned
+    /// before the normalisation (the row then stays unscaled, as :42 returns)
+    pub fn inverse(&self, input: &mut [Complex<f32>], output: &mut [f32]) -> Result<(), FftError> {
+        assert!(output.len() == self.n && input.len() == self.n / 2 + 1, "Fft::inverse: slice lengths");
+        let mut bad: c_int = 0;
+        check(unsafe {
+            ffi::fftconv_fft_inverse_host(self.device, self.n, 1, input.as_ptr() as *const f32, output.as_mut_ptr(),
+                                          &mut bad)
+        });
+        if bad != 0 {
+            return Err(FftError::InputValues(input[0].im != 0.0, input[self.n / 2].im != 0.0));
+        }
+        Ok(())
     }
 }
