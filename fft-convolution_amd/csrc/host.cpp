@@ -1532,21 +1532,120 @@ int lg_tables(int dev, int log2m, LgTab *out) {
     return FFTCONV_OK;
 }
 
+// Bluestein tables of a length n that is not a power of two (the public Fft
+// of any length, launch_fft_bluestein): the chirp w_m = exp(i pi m^2 / n)
+// (m^2 mod 2n in integers, the angle in f64) and the spectrum of the chirp
+// filter b (b_m = b_{P-m} = w_m, m < n) by an f64 FFT on the host, both
+// rounded to f32 once; the filter in the device FFT's bin order.  One set per
+// (device, n), kept for the process.
+constexpr size_t kMaxBluestein = (size_t)1 << 21;  // P = 2^22 at most
+int bluestein_tables(int dev, size_t n, int log2p, const float2 **chirp, const float2 **filt) {
+    static std::mutex mu;
+    static std::map<std::pair<int, size_t>, float2 *> tabs;
+    std::lock_guard<std::mutex> lk(mu);
+    const size_t P = (size_t)1 << log2p;
+    auto it = tabs.find({dev, n});
+    if (it == tabs.end()) {
+        std::vector<double> wr(n), wi(n);
+        for (size_t m = 0; m < n; ++m) {
+            const unsigned long long q = ((unsigned long long)m * m) % (2ull * n);
+            const double ang = M_PI * (double)q / (double)n;
+            wr[m] = std::cos(ang);
+            wi[m] = std::sin(ang);
+        }
+        std::vector<double> br(P, 0.0), bi(P, 0.0);
+        for (size_t m = 0; m < n; ++m) {
+            br[m] = wr[m];
+            bi[m] = wi[m];
+            if (m) {
+                br[P - m] = wr[m];
+                bi[P - m] = wi[m];
+            }
+        }
+        // forward DFT of b in f64: iterative radix-2, exp(-2 pi i / len) per stage
+        for (size_t i = 1, j = 0; i < P; ++i) {
+            size_t bit = P >> 1;
+            for (; j & bit; bit >>= 1) j ^= bit;
+            j ^= bit;
+            if (i < j) {
+                std::swap(br[i], br[j]);
+                std::swap(bi[i], bi[j]);
+            }
+        }
+        for (size_t len = 2; len <= P; len <<= 1) {
+            const size_t h = len / 2;
+            for (size_t k = 0; k < h; ++k) {
+                const double ang = -2.0 * M_PI * (double)k / (double)len;
+                const double c = std::cos(ang), sn = std::sin(ang);
+                for (size_t b0 = 0; b0 < P; b0 += len) {
+                    const size_t u = b0 + k, v = u + h;
+                    const double tr = br[v] * c - bi[v] * sn, ti = br[v] * sn + bi[v] * c;
+                    br[v] = br[u] - tr;
+                    bi[v] = bi[u] - ti;
+                    br[u] += tr;
+                    bi[u] += ti;
+                }
+            }
+        }
+        std::vector<float2> t(n + P);
+        for (size_t m = 0; m < n; ++m) t[m] = make_float2((float)wr[m], (float)wi[m]);
+        for (size_t k = 0; k < P; ++k) {
+            const size_t pos = log2p > kMaxLog2Fused ? lg_position(log2p, k) : k;
+            t[n + pos] = make_float2((float)br[k], (float)bi[k]);
+        }
+        float2 *d = nullptr;
+        HIP_TRY(hipMalloc((void **)&d, t.size() * sizeof(float2)));
+        hipError_t e = hipMemcpy(d, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return fail(FFTCONV_E_DEVICE, std::string("Bluestein tables: ") + hipGetErrorString(e));
+        }
+        it = tabs.emplace(std::make_pair(dev, n), d).first;
+    }
+    *chirp = it->second;
+    *filt = it->second + n;
+    return FFTCONV_OK;
+}
+
 // Fft::forward / inverse on device rows (src/fft_convolver.rs:36-49)
 int fft_rows(int device, size_t n, size_t rows, const float *din, size_t is, float *dout, size_t os, int *status,
              bool inverse, hipStream_t s) {
     if (int r = check_device(device)) return r;
-    if (n < 2 || (n & (n - 1)) || n > ((size_t)2 << kMaxLog2Block))
-        return fail(FFTCONV_E_UNSUPPORTED, "Fft length must be a power of two in 2..2^23 (N = 2 * block)");
-    const size_t cin = inverse ? n + 2 : n, cout = inverse ? n : n + 2;
+    const bool pow2 = n >= 2 && !(n & (n - 1));
+    if (n < 1 || (pow2 && n > ((size_t)2 << kMaxLog2Block)) || (!pow2 && n > kMaxBluestein))
+        return fail(FFTCONV_E_UNSUPPORTED, "Fft length must be 1..2^21, or a power of two up to 2^23");
+    const size_t nbf = 2 * (n / 2 + 1);  // floats of the n/2 + 1 interleaved bins
+    const size_t cin = inverse ? nbf : n, cout = inverse ? n : nbf;
     if (rows > (size_t)INT32_MAX || (rows > 1 && (is < cin || os < cout)))
         return fail(FFTCONV_E_INVALID, "row strides shorter than a row");
     if (rows == 0) return FFTCONV_OK;
     DeviceGuard g(device);
     const float2 *tw = nullptr;
-    if (int r = fft_twiddles(device, ilog2(n), s, &tw)) return r;
+    if (pow2)
+        if (int r = fft_twiddles(device, ilog2(n), s, &tw)) return r;
     FftArgs a{};
     a.in = din; a.in_stride = (long long)is; a.out = dout; a.out_stride = (long long)os; a.tw = tw; a.status = status;
+    if (!pow2) {
+        // any other length: Bluestein over P >= 2n - 1 point FFTs (large.hip)
+        const size_t P = std::max<size_t>(2, next_pow2(2 * n - 1));
+        const int lp = ilog2(P);
+        const float2 *chirp = nullptr, *filt = nullptr, *twP = nullptr;
+        if (int r = bluestein_tables(device, n, lp, &chirp, &filt)) return r;
+        LgTab t{};
+        float2 *scr = nullptr;
+        size_t batch = rows;
+        if (lp > kMaxLog2Fused) {
+            if (int r = lg_tables(device, lp, &t)) return r;
+            batch = std::max<size_t>(1, std::min(rows, ((size_t)64 << 20) / (P * sizeof(float2))));
+            HIP_TRY(hipMallocAsync((void **)&scr, batch * P * sizeof(float2), s));
+        } else {
+            if (int r = fft_twiddles(device, lp + 1, s, &twP)) return r;  // W_{2P}
+        }
+        const hipError_t e = launch_fft_bluestein(n, lp, inverse, a, chirp, filt, twP, t, scr, (int)rows, (int)batch, s);
+        if (scr) HIP_TRY(hipFreeAsync(scr, s));
+        HIP_TRY(e);
+        return FFTCONV_OK;
+    }
     const int log2m = ilog2(n) - 1;
     if (log2m > kMaxLog2Fused) {
         // the long-block passes (large.hip) through a stream-ordered scratch
@@ -1573,7 +1672,8 @@ int fft_rows_host(int device, size_t n, size_t rows, const float *in, float *out
     if (int r = check_device(device)) return r;
     if (rows == 0) return FFTCONV_OK;
     DeviceGuard g(device);
-    const size_t cin = inverse ? n + 2 : n, cout = inverse ? n : n + 2;
+    const size_t nbf = 2 * (n / 2 + 1);
+    const size_t cin = inverse ? nbf : n, cout = inverse ? n : nbf;
     DevPtr<float> din, dout;
     DevPtr<int> dst;
     if (int r = din.alloc(rows * cin)) return r;

@@ -145,12 +145,17 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // FFTCONV_DEBUG_BOUNDS (debug builds only): report out-of-range stream rows
 // and window/state indices with printf instead of touching the memory
 #ifdef FFTCONV_DEBUG_BOUNDS
-#define DBG_CHECK(cond, ...)                                                   \
-    do {                                                                       \
-        if (!(cond)) printf("BOUNDS " __VA_ARGS__);                            \
+// one out-of-line report for every check (a printf inlined at each of the
+// hundreds of inlined load sites made the debug build compile for hours)
+__device__ __attribute__((noinline)) void dbg_bounds(int site, int v0, int v1, int v2, int v3) {
+    printf("BOUNDS site %d blk %d tid %d: %d %d %d %d\n", site, (int)blockIdx.x, (int)threadIdx.x, v0, v1, v2, v3);
+}
+#define DBG_CHECK(cond, site, v0, v1, v2, v3)       \
+    do {                                            \
+        if (!(cond)) dbg_bounds(site, v0, v1, v2, v3); \
     } while (0)
 #else
-#define DBG_CHECK(cond, ...) do {} while (0)
+#define DBG_CHECK(cond, site, v0, v1, v2, v3) do {} while (0)
 #endif
 struct RowStream {
     __amdgpu_buffer_rsrc_t r;
@@ -169,8 +174,7 @@ struct RowStream {
     __device__ __forceinline__ float4 ld4(int voff, int soff) const {
 #ifdef FFTCONV_DEBUG_BOUNDS
         if (voff < nbytes && (soff < 0 || soff + voff + 16 > nbytes)) {
-            printf("BOUNDS ld4 blk %d tid %d voff %d soff %d nbytes %d\n", (int)blockIdx.x, (int)threadIdx.x, voff,
-                   soff, nbytes);
+            dbg_bounds(3, voff, soff, nbytes, 0);  // (site 3: a stream row past the buffer)
             soff = 0;
         }
 #endif

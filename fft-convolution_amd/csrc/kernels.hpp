@@ -264,6 +264,14 @@ hipError_t launch_ir_large(int log2b, const IrArgs &a, const LgTab &t, int chann
 // scratch [batch][N/2] complex
 hipError_t launch_fft_large(int log2m, bool inverse, const FftArgs &a, const LgTab &t, float2 *scratch, int rows,
                             int batch, hipStream_t s);
+// the public Fft of a length n that is not a power of two: Bluestein over
+// P = 2^log2p >= 2n - 1 point FFTs (large.hip).  chirp[m] = exp(i pi m^2 / n)
+// (m < n); filt = FFT_P of the chirp filter (natural order for P <= 8192,
+// else the four-step's transposed order); twP = W_{2P}^i (P <= 8192); t =
+// the four-step tables of P (P > 8192); scratch [batch][P] (P > 8192)
+hipError_t launch_fft_bluestein(size_t n, int log2p, bool inverse, const FftArgs &a, const float2 *chirp,
+                                const float2 *filt, const float2 *twP, const LgTab &t, float2 *scratch, int rows,
+                                int batch, hipStream_t s);
 // crossfade mix of calls longer than the in-LDS walk (n > 1024): the walk
 // once into a device table (one lane), then the mix reading it
 hipError_t launch_crossfade_walk(const CrossfadeMixArgs &a, float *vtab, hipStream_t s);

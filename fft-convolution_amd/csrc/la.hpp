@@ -165,7 +165,7 @@ __device__ __forceinline__ void la_group(int lv, int g, int act, int &lo, int &h
 __device__ __forceinline__ float4 *la_win(const ProcArgs &a, int jb, size_t c, int win, int lv, int pos, int B) {
 #ifdef FFTCONV_DEBUG_BOUNDS
     if (!(c < (size_t)a.la_channels && win >= 0 && win < 2 && lv >= 1 && lv <= 3 && pos >= 0 && pos < la_per(lv))) {
-        printf("BOUNDS la_win blk %d c %d win %d lv %d pos %d\n", (int)blockIdx.x, (int)c, win, lv, pos);
+        dbg_bounds(4, (int)c, win, lv, pos);  // (site 4: a window row index)
         c = 0; win = 0; lv = 1; pos = 0;
     }
 #endif
@@ -302,7 +302,7 @@ template <int LOG2B>
 __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c, int lv, int &cur, int &act, int &win,
                                                 int &d) {
     const ProcJob &J = a.job[jb];
-    DBG_CHECK(c >= 0 && c < a.la_channels, "anchor state blk %d c %d lv %d\n", (int)blockIdx.x, c, lv);
+    DBG_CHECK(c >= 0 && c < a.la_channels, 1, c, lv, a.la_channels, 0);  // (site 1: an anchor's channel)
     const int4 st = J.state[c];
     const int sx = __builtin_amdgcn_readfirstlane(st.x), sy = __builtin_amdgcn_readfirstlane(st.y);
     const int sz = __builtin_amdgcn_readfirstlane(st.z), sw = __builtin_amdgcn_readfirstlane(st.w);
@@ -661,8 +661,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         const ProcJob &JC = JK(k);
         const size_t c = (size_t)CS(k);
         const int cur = __builtin_amdgcn_readfirstlane(ST(k).x);
-        DBG_CHECK(c < (size_t)a.la_channels && cur >= 0 && cur < J.S, "step chain blk %d c %d cur %d nvalid %d\n",
-                  (int)blockIdx.x, (int)c, cur, nvalid);
+        DBG_CHECK(c < (size_t)a.la_channels && cur >= 0 && cur < J.S, 2, (int)c, cur, nvalid, 0);  // (site 2: a step chain)
         float2 *bufA = reinterpret_cast<float2 *>(chan_lds(k));
         float2 *bufB = bufA + B;
         float *p0l = reinterpret_cast<float *>(bufA + 3 * B), *p1l = p0l + B;

@@ -700,6 +700,178 @@ hipError_t lg_fft_t(bool inverse, const FftArgs &a, const LgTab &t, float2 *scra
     return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------
+// Fft of any length n (src/fft_convolver.rs:29-49; realfft plans every
+// length, RealToComplexOdd / Even over rustfft's mixed-radix, Rader and
+// Bluestein plans).  Here every non-power-of-two n runs Bluestein's chirp-z
+// transform over the power-of-two complex FFTs above:
+//   X[k] = conj(w_k) sum_j (s_j conj(w_j)) w_(k-j),  w_m = exp(i pi m^2 / n),
+// the circular convolution of length P = 2^LP >= 2n - 1 as FFT, product with
+// the chirp filter's spectrum Bf (f64 on the host, rounded), inverse FFT.
+// P <= 8192: one workgroup per row in LDS (natural order); larger P: the
+// four-step passes, with the spectra (A and Bf) in the transposed order.
+// Forward: s = x (real), bins 0..n/2 out, DC (and an even n's Nyquist)
+// imaginary part exactly 0.  Inverse: s = conj of the Hermitian spectrum
+// (DC / Nyquist imaginary parts taken as 0, flagged as FftError::InputValues),
+// out = Re(DFT(s)) / n -- divided, as Fft::inverse (:44-46), unless flagged.
+// ---------------------------------------------------------------------------
+struct BsPass {
+    int n, inverse;
+    const float *in;
+    long long in_stride;
+    float *out;
+    long long out_stride;
+    int *status;
+    const float2 *w;    // [n] chirp
+    const float2 *bf;   // [P] filter spectrum
+    const float2 *twP;  // W_{2P}^i, i < 2P (one-workgroup FFT)
+    LgTab tb;           // four-step tables of P (twM = W_P^j)
+    float2 *Y;          // [rows][P] scratch (four-step)
+    int row0;
+};
+
+// s_j of row r: the sequence whose forward DFT is wanted
+__device__ __forceinline__ float2 bs_src(const BsPass &p, const float *in, int j) {
+    if (!p.inverse) return make_float2(in[j], 0.f);
+    const int nb = p.n / 2;  // last bin
+    // conj(X_full[j]): X_full[j] = bin j (j <= n/2) or conj(bin n - j)
+    if (j <= nb) {
+        const bool real = j == 0 || (2 * j == p.n);  // DC / Nyquist: imaginary part taken as 0
+        return make_float2(in[2 * j], real ? 0.f : -in[2 * j + 1]);
+    }
+    return make_float2(in[2 * (p.n - j)], in[2 * (p.n - j) + 1]);
+}
+__device__ __forceinline__ bool bs_flagged(const BsPass &p, const float *in) {
+    return p.inverse && (in[1] != 0.f || (p.n % 2 == 0 && in[p.n + 1] != 0.f));
+}
+// X_m = conj(w_m) c_m / P written out (forward: bins m <= n/2; inverse: sample m)
+__device__ __forceinline__ void bs_out(const BsPass &p, float *o, int m, float2 c, float invP, bool flagged) {
+    const float2 x = cmulc(make_float2(c.x * invP, c.y * invP), p.w[m]);
+    if (!p.inverse) {
+        if (2 * m > p.n) return;
+        const bool real = m == 0 || 2 * m == p.n;
+        o[2 * m] = x.x;
+        o[2 * m + 1] = real ? 0.f : x.y;
+    } else {
+        o[m] = flagged ? x.x : x.x / (float)p.n;
+    }
+}
+
+template <int LP>
+__global__ __launch_bounds__(LG_NT) void bs_small(BsPass p) {
+    constexpr int P = 1 << LP;
+    constexpr float invP = 1.0f / (float)P;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + P;
+    const int tid = threadIdx.x;
+    const size_t r = p.row0 + blockIdx.x;
+    const float *in = p.in + r * p.in_stride;
+    for (int j = tid; j < P; j += LG_NT) b0[j] = j < p.n ? cmulc(bs_src(p, in, j), p.w[j]) : make_float2(0.f, 0.f);
+    __syncthreads();
+    float2 *A = bfft<LP, 1, false, false>(b0, b1, p.twP, tid);
+    float2 *Bq = A == b0 ? b1 : b0;
+    for (int k = tid; k < P; k += LG_NT) Bq[k] = cmul(A[k], p.bf[k]);
+    __syncthreads();
+    const float2 *c = bfft<LP, 1, false, true>(Bq, A, p.twP, tid);
+    const bool flagged = bs_flagged(p, in);
+    if (p.status && tid == 0) p.status[r] = flagged ? 1 : 0;
+    float *o = p.out + r * p.out_stride;
+    for (int m = tid; m < p.n; m += LG_NT) bs_out(p, o, m, c[m], invP, flagged);
+}
+
+// four-step, pass A: pre-chirp, column FFTs, x W_P^(n2 k1) -> Y
+template <int LP>
+__global__ __launch_bounds__(LG_NT) void bs_cols_fwd(BsPass p) {
+    using G = LgGeo<LP>;
+    constexpr int M2 = G::M2, TC = G::TC, P = G::M;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + LG_E;
+    const int tid = threadIdx.x, c0 = (int)(blockIdx.x % G::NTILE) * TC;
+    const size_t row = blockIdx.x / G::NTILE;
+    const float *in = p.in + (p.row0 + row) * p.in_stride;
+    for (int e = tid; e < LG_E; e += LG_NT) {
+        const int j = (e / TC) * M2 + c0 + (e & (TC - 1));
+        b0[e] = j < p.n ? cmulc(bs_src(p, in, j), p.w[j]) : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    const float2 *R = bfft<G::L1, TC, true, false>(b0, b1, p.tb.twA, tid);
+    float2 *Y = p.Y + row * P;
+    for (int e = tid; e < LG_E; e += LG_NT) {
+        const int t = e & (TC - 1), k1 = e / TC, n2 = c0 + t;
+        Y[(size_t)k1 * M2 + n2] = cmul(R[e], p.tb.twM[(n2 * k1) & (P - 1)]);
+    }
+}
+
+// pass B: one row k1: row FFT, x Bf (transposed order), inverse row FFT,
+// x W_P^-(n2 k1), in place
+template <int LP>
+__global__ __launch_bounds__(LG_NT) void bs_rows(BsPass p) {
+    using G = LgGeo<LP>;
+    constexpr int M1 = G::M1, M2 = G::M2, P = G::M;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + M2;
+    const int tid = threadIdx.x, k1 = (int)(blockIdx.x % M1);
+    const size_t row = blockIdx.x / M1;
+    float2 *Y = p.Y + row * P + (size_t)k1 * M2;
+    for (int e = tid; e < M2; e += LG_NT) b0[e] = Y[e];
+    __syncthreads();
+    float2 *F = bfft<G::L2, 1, false, false>(b0, b1, p.tb.twB, tid);
+    float2 *Gb = F == b0 ? b1 : b0;
+    for (int e = tid; e < M2; e += LG_NT) Gb[e] = cmul(F[e], p.bf[(size_t)k1 * M2 + e]);
+    __syncthreads();
+    const float2 *R = bfft<G::L2, 1, false, true>(Gb, F, p.tb.twB, tid);
+    for (int e = tid; e < M2; e += LG_NT) Y[e] = cmulc(R[e], p.tb.twM[(e * k1) & (P - 1)]);
+}
+
+// pass C: inverse column FFTs -> c_m, m = M2 n1 + n2; post-chirp and out
+template <int LP>
+__global__ __launch_bounds__(LG_NT) void bs_cols_inv(BsPass p) {
+    using G = LgGeo<LP>;
+    constexpr int M2 = G::M2, TC = G::TC, P = G::M;
+    constexpr float invP = 1.0f / (float)P;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + LG_E;
+    const int tid = threadIdx.x, c0 = (int)(blockIdx.x % G::NTILE) * TC;
+    const size_t row = blockIdx.x / G::NTILE;
+    const float2 *V = p.Y + row * P;
+    for (int e = tid; e < LG_E; e += LG_NT) b0[e] = V[(size_t)(e / TC) * M2 + c0 + (e & (TC - 1))];
+    __syncthreads();
+    const float2 *R = bfft<G::L1, TC, true, true>(b0, b1, p.tb.twA, tid);
+    const size_t r = p.row0 + row;
+    const float *in = p.in + r * p.in_stride;
+    const bool flagged = bs_flagged(p, in);
+    if (p.status && blockIdx.x % G::NTILE == 0 && tid == 0) p.status[r] = flagged ? 1 : 0;
+    float *o = p.out + r * p.out_stride;
+    for (int e = tid; e < LG_E; e += LG_NT) {
+        const int m = (e / TC) * M2 + c0 + (e & (TC - 1));
+        if (m < p.n) bs_out(p, o, m, R[e], invP, flagged);
+    }
+}
+
+template <int LP>
+hipError_t bs_launch_t(const BsPass &p0, int rows, int batch, hipStream_t s) {
+    if constexpr (LP <= 13) {
+        constexpr size_t lds = 2 * ((size_t)1 << LP) * sizeof(float2);
+        if (hipError_t e = lds_attr(bs_small<LP>, lds); e != hipSuccess) return e;
+        BsPass p = p0;
+        p.row0 = 0;
+        hipLaunchKernelGGL(bs_small<LP>, dim3(rows), dim3(LG_NT), lds, s, p);
+        return hipGetLastError();
+    } else {
+        using G = LgGeo<LP>;
+        for (int r0 = 0; r0 < rows; r0 += batch) {
+            const int nr = std::min(batch, rows - r0);
+            BsPass p = p0;
+            p.row0 = r0;
+            hipLaunchKernelGGL(bs_cols_fwd<LP>, dim3(nr * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
+            hipLaunchKernelGGL(bs_rows<LP>, dim3(nr * G::M1), dim3(LG_NT), 2 * (size_t)G::M2 * sizeof(float2), s, p);
+            hipLaunchKernelGGL(bs_cols_inv<LP>, dim3(nr * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+}
+
 }  // namespace
 
 #define LG_DISPATCH(FN, LM, ...)                     \
@@ -743,6 +915,33 @@ hipError_t launch_fft_large(int log2m, bool inverse, const FftArgs &a, const LgT
                             int batch, hipStream_t s) {
     if (rows <= 0) return hipSuccess;
     LG_DISPATCH(lg_fft_t, log2m, inverse, a, t, scratch, rows, batch, s)
+}
+
+hipError_t launch_fft_bluestein(size_t n, int log2p, bool inverse, const FftArgs &a, const float2 *chirp,
+                                const float2 *filt, const float2 *twP, const LgTab &t, float2 *scratch, int rows,
+                                int batch, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    if (n < 1 || n > INT32_MAX) return hipErrorInvalidValue;
+    BsPass p{};
+    p.n = (int)n;
+    p.inverse = inverse ? 1 : 0;
+    p.in = a.in;
+    p.in_stride = a.in_stride;
+    p.out = a.out;
+    p.out_stride = a.out_stride;
+    p.status = a.status;
+    p.w = chirp;
+    p.bf = filt;
+    p.twP = twP;
+    p.tb = t;
+    p.Y = scratch;
+    switch (log2p) {
+#define BSC(L) case L: return bs_launch_t<L>(p, rows, batch, s);
+        BSC(1) BSC(2) BSC(3) BSC(4) BSC(5) BSC(6) BSC(7) BSC(8) BSC(9) BSC(10) BSC(11) BSC(12) BSC(13)
+        BSC(14) BSC(15) BSC(16) BSC(17) BSC(18) BSC(19) BSC(20) BSC(21) BSC(22)
+#undef BSC
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace fftconv

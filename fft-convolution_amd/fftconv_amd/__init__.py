@@ -217,7 +217,9 @@ def device_count() -> int:
 
 class Fft:
     """Fft (src/fft_convolver.rs:7-50) of length n on the GPU: realfft's
-    R2C / C2R (forward unnormalised, inverse / n), batched over rows."""
+    R2C / C2R (forward unnormalised, inverse / n), batched over rows.  Any n in
+    1..2^21 (Bluestein for a length that is not a power of two), or a power of
+    two up to 2^23."""
 
     def __init__(self, length: int, device: int = 0):
         self.n = int(length)
@@ -228,7 +230,7 @@ class Fft:
         x = _f32(x)
         flat = x.ndim == 1
         x2 = x.reshape(-1, self.n)
-        out = np.zeros((x2.shape[0], self.n + 2), np.float32)
+        out = np.zeros((x2.shape[0], 2 * (self.n // 2 + 1)), np.float32)
         _check(lib().fftconv_fft_forward_host(self.device, self.n, x2.shape[0], _p(x2), _p(out)))
         out = out.view(np.complex64)
         return out[0] if flat else out
