@@ -1892,15 +1892,25 @@ LaDims la_dims(int log2b, int S) {
 // anchor workgroups of a launch (ProcArgs::la_n): per level the scheduled
 // channels of [c0, C) -- all of them when la_all > 0 -- in whole XCD rounds
 // of 8 for the level 2/3 anchors (la_anchor_far)
-static void la_counts(ProcArgs &a, int log2b, int S, int C, bool all, bool mid_wg) {
+// fold (ProcArgs::la_l1in2): level-1 anchors ride in the level-2 anchor
+// workgroups (one each, after the level-2 walk), so the level-2 count covers
+// the level-1 channels too.
+static void la_counts(ProcArgs &a, int log2b, int S, int C, bool all, bool mid_wg, bool fold = false) {
     const LaDims d = la_dims(log2b, S);
+    int n1 = 0;
     for (int lv = 1; lv <= 3; ++lv) {
         const int P = d.per[lv - 1];
         const int t0 = a.la_t % P;
         const int n = all ? C - a.la_c0 : (C > t0 ? (C - t0 + P - 1) / P : 0);
-        if (lv == 1) a.la_n[0] = mid_wg ? (n + 7) / 8 * 8 : 0;  // (whole rounds of 8: the XF 3 grid interleave)
-        else a.la_n[lv - 1] = (lv <= d.nlv) ? (n + 7) / 8 * 8 * d.wg[lv - 1] : 0;
+        if (lv == 1) {
+            n1 = n;
+            a.la_n[0] = mid_wg ? (n + 7) / 8 * 8 : 0;  // (whole rounds of 8: the XF 3 grid interleave)
+        } else {
+            a.la_n[lv - 1] = (lv <= d.nlv) ? (n + 7) / 8 * 8 * d.wg[lv - 1] : 0;
+        }
     }
+    if (fold) a.la_n[1] = std::max(a.la_n[1], (n1 + 7) / 8 * 8);
+    a.la_l1in2 = fold ? 1 : 0;
     a.la_nlv = d.nlv;
 }
 
@@ -1937,7 +1947,12 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         args.la_rebuild = 0;
         args.la_t = a.la_t % LA_PER;
         if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_LAFULL)) args.la_all = -1;  // no anchors: every eligible step sums all its rows
-        la_counts(args, LOG2B, a.job[0].S, channels, args.la_all > 0, !LaStep<LOG2B>::MIDIN);
+        // standalone batches at B <= 256: level 1 in the level-2 anchor
+        // workgroups (they finish their walks first); the crossfade launches
+        // keep it in the step workgroups (LaStep::MIDIN)
+        const bool fold = a.la_mix == 0 && LOG2B <= LA_MIDIN_MAXLOG;
+        const bool midin = !fold && LOG2B <= LA_MIDIN_MAXLOG;
+        la_counts(args, LOG2B, a.job[0].S, channels, args.la_all > 0, !fold && !midin, fold);
         if (args.la_all < 0) args.la_n[0] = args.la_n[1] = args.la_n[2] = 0;
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1961,7 +1976,7 @@ hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStre
 int la_trace_grid(int log2b, int S, int channels) {  // (steady-state launches: la_t = 0 has the most anchors)
     if (log2b < 7 || log2b > 9) return 0;
     ProcArgs a{};
-    la_counts(a, log2b, S, channels, false, true);
+    la_counts(a, log2b, S, channels, false, true, true);
     return 2 * (a.la_n[0] + a.la_n[1] + a.la_n[2]) + channels + LA_XWG;  // (XF 3: A's and B's anchors)
 }
 

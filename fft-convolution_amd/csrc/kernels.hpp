@@ -127,6 +127,7 @@ struct ProcArgs {
     int la_t;              // launch counter mod LA_PER: channel c anchors at period P when (c - t) % P == 0
     int la_seq;            // 1 or 2, alternating per lookahead launch; 0 in every other launch
     int la_channels;       // channels of the batch (step workgroups cover LaStep::NCH each)
+    int la_l1in2;          // 1: level-1 anchor b runs in level-2 anchor workgroup b, after its walk
     // crossfade on the lookahead step (CrossfadeConvolver::process :72-77):
     // 1 = A's launch also writes this call's per-sample mix selectors to mix_tab;
     // 2 = B's launch mixes in its epilogue: out = mix(mix.buf_a, B's block);

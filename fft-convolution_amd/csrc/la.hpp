@@ -453,7 +453,8 @@ struct LaStep {
     // after the pre) also run the level-1 anchors of its channels, after the
     // pre, under the transform chains; B = 512 launches level-1 anchor
     // workgroups
-    static constexpr bool MIDIN = LOG2B <= LA_MIDIN_MAXLOG;
+    // (XF 0: level 1 in the level-2 anchor workgroups instead, la_l1in2)
+    static constexpr bool MIDIN = LOG2B <= LA_MIDIN_MAXLOG && XF != 0;
     static constexpr bool NEARNEXT = LOG2B >= LA_NEARNEXT_MINLOG;
     // tw (the 3N/4 = 1.5B float2 the transforms index) | per channel:
     // bufA | bufB | pre (float2) | tail0 | tail1 (float) -- H[0] and the
@@ -1039,6 +1040,10 @@ __device__ __forceinline__ bool la_anchor(const ProcArgs &a, int jb, int ba, uns
     ba -= a.la_n[2];
     if (ba < a.la_n[1]) {
         la_anchor_far<LOG2B, 2, NTL>(a, jb, ba, smem);
+        // level-1 anchor ba after the level-2 walk: the level-2 workgroups
+        // finish first (r4 timeline: 8.9 us median against 13.4 for level 3
+        // and ~15 for the in-step level-1 walks they replace)
+        if (a.la_l1in2) la_anchor_mid<LOG2B>(a, jb, ba);
         return true;
     }
     ba -= a.la_n[1];
