@@ -768,6 +768,9 @@ struct TwoStageCore {
             k = (int)std::lround(per_b / std::max(tail_b, 1.0));
             k = std::min(8, std::max(2, k));
         }
+        // (tuning, read once per handle at creation: FFTCONV_TAIL_CU_DIV=k
+        // overrides the share, 1 = unmasked)
+        if (const char *e = getenv("FFTCONV_TAIL_CU_DIV")) k = std::max(1, atoi(e));
         int ncu = 0;
         HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         if (k <= 1 || ncu <= 0) {

@@ -478,6 +478,10 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     Acc2 acc[SPL];
 #pragma unroll
     for (int s = 0; s < SPL; ++s) acc[s].zero();
+    constexpr int CNB = (B + 63) / 64;  // the chain's samples per lane
+    float ovr[CNB], p0r[CNB], p1r[CNB];
+#pragma unroll
+    for (int i = 0; i < CNB; ++i) ovr[i] = p0r[i] = p1r[i] = 0.f;
     if (wave == 0) {
         // ---- critical chain, one wave ----
         dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);   // x[0..B) as packed z[0..B/2)
@@ -486,11 +490,21 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         dma_16b<64>(h0l, Hc, B * (int)sizeof(float2));
         if (act > 1) dma_16b<64>(h1l, Hc + B, B * (int)sizeof(float2));
         dma_16b<64>(prel, prec, B * (int)sizeof(float2));
-        dma_f32<64>(ovl, ovc, B);
-        if (J.add0) dma_f32<64>(p0l, J.add0 + c * J.add_stride, B);
-        if (J.add1) dma_f32<64>(p1l, J.add1 + c * J.add_stride, B);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
+        // the overlap and the two-stage adds are read only by the overlap-add
+        // at the chain's end: plain loads issued now arrive under the
+        // transforms, instead of holding the R2C behind the prologue wait
+        // (cfg3 head: the adds come from the tail buffers, HBM-cold)
+#pragma unroll
+        for (int i = 0; i < CNB; ++i) {
+            const int j = lane + 64 * i;
+            if (j < B) {
+                ovr[i] = ovc[j];
+                if (J.add0) p0r[i] = J.add0[c * J.add_stride + j];
+                if (J.add1) p1r[i] = J.add1[c * J.add_stride + j];
+            }
+        }
         proc_stamp(a, 0);
         if (J.tin) {  // two-stage: append the block to tail_input (:459-461)
             const float *xb = reinterpret_cast<const float *>(bufA);
@@ -544,11 +558,14 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             for (int m = lane; m < B; m += 64) Q[m] = real_pre<LOG2B, 64>(Z, m, twl);
             wave_sync();
             const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(Q, Z, twl));
-            for (int j = lane; j < B; j += 64) {  // overlap-add (:270-274) + two-stage adds (:439-454)
-                float v = y[j] * invN + ovl[j];
+#pragma unroll
+            for (int i = 0; i < CNB; ++i) {  // overlap-add (:270-274) + two-stage adds (:439-454)
+                const int j = lane + 64 * i;
+                if (j >= B) continue;
+                float v = y[j] * invN + ovr[i];
                 if (J.add0) {
-                    v += p0l[j];
-                    if (J.add1) v += p1l[j];
+                    v += p0r[i];
+                    if (J.add1) v += p1r[i];
                 }
                 outc[j] = v;
                 ovc[j] = y[B + j] * invN;  // :283-284
@@ -557,11 +574,14 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             // output.fill(0); return (:264-267): the block stays in the input
             // buffer, fill / current unchanged, pre still describes this block
             float *ibc = J.inbuf + c * B;
-            for (int j = lane; j < B; j += 64) {
+#pragma unroll
+            for (int i = 0; i < CNB; ++i) {
+                const int j = lane + 64 * i;
+                if (j >= B) continue;
                 float v = 0.f;
                 if (J.add0) {
-                    v += p0l[j];
-                    if (J.add1) v += p1l[j];
+                    v += p0r[i];
+                    if (J.add1) v += p1r[i];
                 }
                 outc[j] = v;
                 ibc[j] = inc[j];
