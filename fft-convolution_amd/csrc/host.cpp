@@ -286,6 +286,14 @@ struct UniformCore {
     DevPtr<float2> lg_v;
     LgTab lgt{};
     bool lg_whole = true;
+    // far-row windows of the generic step (1024 <= B <= 8192):
+    // standalone batches and the two-stage tail (gw_ok, set before init);
+    // gw_p = the split row (0 = off), gwin = [C][P][B], gw_t = one-block
+    // steps so far (the anchor class of the next one)
+    bool gw_ok = false;
+    int gw_p = 0;
+    DevPtr<float2> gwin;
+    unsigned long long gw_t = 0;
 
     ~UniformCore() {
         if (stream) {
@@ -340,6 +348,9 @@ struct UniformCore {
             if (int r = hstage.alloc(C * ir_len, ir_len)) return r;
         if (large)
             if (int r = alloc_large()) return r;
+        gw_p = gw_ok && gw_supported(log2b, (int)S) ? kGwP : 0;
+        if (gw_p)
+            if (int r = gwin.alloc(C * (size_t)gw_p * B)) return r;
         la_W = la_ok ? la_parts(log2b, (int)S) : 0;
         if (la_W) {
             const LaDims d = la_dims(log2b, (int)S);
@@ -603,6 +614,17 @@ struct UniformCore {
             ++la_t;
         }
         lg_fill(a, n);
+        a.gw_p = gw_p;  // (every launch: the split order)
+        if (gw_p && n == B && gw_windows_allowed()) {
+            // a one-block step reads the live windows, then the channels of
+            // class gw_t mod P anchor theirs for their next P blocks
+            a.gw = gwin.p;
+            a.gw_t = (int)(gw_t % (unsigned long long)gw_p);
+            HIP_TRY(launch_process(log2b, a, (int)C, s));
+            HIP_TRY(launch_gw_anchor(log2b, a, (int)C, s));
+            ++gw_t;
+            return FFTCONV_OK;
+        }
         HIP_TRY(launch_process(log2b, a, (int)C, s));
         return FFTCONV_OK;
     }
@@ -643,6 +665,8 @@ struct UniformCore {
         if (int r = cp(state, o.state)) return r;
         if (int r = cp(laW, o.laW)) return r;
         la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
+        if (int r = cp(gwin, o.gwin)) return r;
+        gw_ok = o.gw_ok; gw_p = o.gw_p; gw_t = o.gw_t;
         large = o.large;
         if (large) {  // (the progress words are zero between calls)
             if (int r = alloc_large()) return r;
@@ -872,6 +896,7 @@ struct TwoStageCore {
             tail.reset(new (std::nothrow) UniformCore());
             if (!tail) return fail(FFTCONV_E_NOMEM, "out of host memory");
             tail->parent_stream = stream;
+            tail->gw_ok = true;  // one full-block call per period: far-row windows
             st = slice(2 * T, tl, tmp);
             if (int r = tail->init(dev, C, tmp.data(), tl, st, T, tl)) return r;
         }
@@ -1760,7 +1785,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 511 || variant < -1) return fail(FFTCONV_E_INVALID, "variant must be 0..511 (or -1 = auto)");
+    if (variant > 2047 || variant < -1) return fail(FFTCONV_E_INVALID, "variant must be 0..2047 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }
@@ -1790,6 +1815,7 @@ fftconv_uniform *fftconv_uniform_init_batch(int device, size_t channels, const f
     auto *h = new (std::nothrow) fftconv_uniform();
     if (!h) { set_error("out of host memory"); return nullptr; }
     h->core.la_ok = true;
+    h->core.gw_ok = true;
     h->core.own_stage = true;
     int r = h->core.init(device, channels, responses, response_len, response_stride, max_block_size,
                          max_response_length);
@@ -1865,6 +1891,7 @@ int fftconv_uniform_synchronize(fftconv_uniform *h) {
 }
 size_t fftconv_uniform_channels(const fftconv_uniform *h) { return h ? h->core.C : 0; }
 int fftconv_uniform_lookahead_parts(const fftconv_uniform *h) { return h ? h->core.la_W : 0; }
+int fftconv_uniform_far_windows(const fftconv_uniform *h) { return h ? h->core.gw_p : 0; }
 size_t fftconv_uniform_block_size(const fftconv_uniform *h) { return h ? h->core.B : 0; }
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h) { return h ? h->core.S : 0; }
 int fftconv_uniform_ir_spectrum(const fftconv_uniform *h, size_t channel, size_t segment, float *out) {

@@ -90,6 +90,17 @@ template <int VEC> using AccT = std::conditional_t<VEC == 2, Acc2, Acc1>;
 
 __device__ __forceinline__ float4 vadd(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 __device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+// streaming accesses (nontemporal): rows used once, which must not evict the
+// working set of latency-bound launches running beside them (a two-stage head)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ntld4(const float4 *p) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void ntst4(float4 *p, float4 v) {
+    const f32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f32x4 *>(p));
+}
 
 // conv = pre + x (.) h for one slot, packed-aware (slot 0 bin 0 is (DC, Nyquist)).
 __device__ __forceinline__ float4 slot_mac(float4 pre, float4 x, float4 h, int slot) {
@@ -196,14 +207,14 @@ struct RowStream {
     __device__ __forceinline__ float2 ld(int voff, int soff, float2 *) const { return ld2<NTL>(voff, soff); }
 };
 
-// pre_multiplied = sum_{i=1}^{act-1} H[i] (.) X[(cur+i) % act] over this
-// thread's slots (src/fft_convolver.rs:244-255).  Rows i = 1..act-1 are
-// visited in scan order t = 0..act-2, group g taking t = g (mod G).
-// ZZ: every other block scans the rows backwards (rows read last by one step
-// are read first by the next).  NTL: nontemporal loads.
+// pre_multiplied = sum_{i=i0}^{i1-1} H[i] (.) X[(cur+i) % act] over this
+// thread's slots (src/fft_convolver.rs:244-255; the whole sum is rows
+// 1..act-1).  The rows are visited in scan order t = 0..i1-i0-1, group g
+// taking t = g (mod G).  ZZ: every other block scans the rows backwards (rows
+// read last by one step are read first by the next).  NTL: nontemporal loads.
 template <int LOG2B, int NT, bool ZZ, bool NTL, class AccArr>
 __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const float2 *Xc, int S, int cur, int act,
-                                         int flags, int f0, int g) {
+                                         int i0, int i1, int flags, int f0, int g) {
     using Gm = Geo<LOG2B, NT>;
     constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT, U = Gm::U;
     constexpr int ROWB = B * (int)sizeof(float2);  // bytes per row
@@ -216,10 +227,11 @@ __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const fl
     for (int s = 0; s < SPT; ++s) acc[s].zero();
     const bool rev = ZZ && (flags & FLAG_REV);
     const int di = rev ? -G : G;
+    const int nr = i1 - i0;
     int t = g;
-    int i = rev ? act - 1 - t : 1 + t;
+    int i = rev ? i1 - 1 - t : i0 + t;
     int xi = (cur + i) % act;  // index_audio = (current + i) % active
-    for (; t + (U - 1) * G < act - 1; t += U * G) {
+    for (; t + (U - 1) * G < nr; t += U * G) {
         vec_t hv[U][SPT], xv[U][SPT];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -240,7 +252,7 @@ __device__ __forceinline__ void mac_rows(AccArr &acc, const float2 *Hc, const fl
 #pragma unroll
             for (int s = 0; s < SPT; ++s) acc[s].mac(hv[u][s], xv[u][s]);
     }
-    for (; t < act - 1; t += G) {
+    for (; t < nr; t += G) {
         const int ho = i * ROWB, xo = xi * ROWB;
 #pragma unroll
         for (int s = 0; s < SPT; ++s) {
@@ -718,6 +730,13 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
     // the common call: exactly one full block from an empty input buffer
     const bool one_block = PF && fill == 0 && n == B && !(flags & FLAG_INBUF);
     const bool epi = J.add0 != nullptr || J.tin != nullptr;
+    // far-row windows (B >= 1024): pre_multiplied is summed as
+    // rows 1..sp-1 plus rows sp..act-1, in every launch of such a batch, so
+    // the result does not depend on which steps read a window; a one-block
+    // call of a channel whose window is live reads the far part from it
+    constexpr bool GW = G == 1 && VEC == 2 && !ZZ && LOG2B >= 10;
+    const int sp = GW && a.gw_p > 0 && act > a.gw_p ? a.gw_p : 0;
+    const bool gwin = sp && a.gw && fill == 0 && n == B && !(flags & (FLAG_INBUF | FLAG_PRE)) && (flags & FLAG_GW);
     if constexpr (PF) {
         dma_16b<NT>(twl, a.tw, 2 * B * (int)sizeof(float2));
         if constexpr (B >= 2) dma_16b<NT>(h0l, Hc, B * (int)sizeof(float2));
@@ -767,8 +786,25 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
             }
         } else if (was_empty) {                                          // :244-255
             AccT<VEC> acc[SPT];
-            mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, J.S, cur, act, flags, f0, g);
-            if constexpr (G > 1) {
+            mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, J.S, cur, act, 1, sp ? sp : act, flags, f0, g);
+            if constexpr (GW) {
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) pacc[s] = acc[s].get(f0 + s * NT);
+                // far rows sp..act-1: this block's window row (the anchor
+                // summed them, gw_anchor_kernel), else summed here; near +
+                // far either way
+                if (gwin) {
+                    const int k = (int)(((long long)a.gw_t - 1 - (long long)c) % sp + sp) % sp;
+                    DBG_CHECK(k >= 0 && k < sp, 40, k, a.gw_t, sp, (int)c);
+                    const float4 *wr = reinterpret_cast<const float4 *>(a.gw + ((size_t)c * sp + k) * B);
+#pragma unroll
+                    for (int s = 0; s < SPT; ++s) pacc[s] = vadd(pacc[s], ntld4(wr + f0 + s * NT));
+                } else if (sp) {  // (acc reused: one accumulator set live)
+                    mac_rows<LOG2B, NT, ZZ, NTL>(acc, Hc, Xc, J.S, cur, act, sp, act, flags, f0, g);
+#pragma unroll
+                    for (int s = 0; s < SPT; ++s) pacc[s] = vadd(pacc[s], acc[s].get(f0 + s * NT));
+                }
+            } else if constexpr (G > 1) {
                 red[g * F + f0] = acc[0].get(f0);
                 __syncthreads();
                 if (owner) {
@@ -895,8 +931,79 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
 #pragma unroll
         for (int s = 0; s < SPT; ++s) reinterpret_cast<vec_t *>(prec)[f0 + s * NT] = pacc[s];
     }
-    if (tid == 0) J.state[c] = make_int4(cur, act, fill, la_clear(flags, a));
+    // (a live window stays live only across a step that read it and advanced)
+    if (tid == 0) J.state[c] = make_int4(cur, act, fill, la_clear(flags, a) | (gwin && !err ? FLAG_GW : 0));
     if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
+}
+
+// ---------------------------------------------------------------------------
+// Far-row windows of the generic step (B >= 1024).  After step t
+// of a batch, the channels of class t mod P (c = t mod P + P j) sum, for each
+// of their next P blocks k = 0..P-1 (current = cur' - k, cur' = the state
+// after step t), the far rows
+//   W[k] = sum_{i=P}^{act-1} H[i] (.) X[(cur' - k + i) % act]
+// (src/fft_convolver.rs:244-255 restricted to i >= P): rows written by block t
+// or earlier, still in the ring at block t+1+k.  One pass over the far rows
+// serves all P windows -- each X row meets P IR rows from a register ring.
+// Each window accumulates its rows in the step's order with the step's
+// arithmetic (Acc2), so near + W is bit-identical to the step summing the
+// far rows itself.  A workgroup: one channel, 256 slots (512 bins).  Channels
+// whose ring is off the block path (a buffered partial block, a failed C2R)
+// or too short get no window: FLAG_GW cleared.
+template <int LOG2B>
+__global__ __launch_bounds__(256) void gw_anchor_kernel(ProcArgs a) {
+    constexpr int B = 1 << LOG2B, F = B / 2, P = kGwP;
+    const ProcJob &J = a.job[0];
+    const int cls = a.gw_t % P;
+    const int c = cls + P * (int)blockIdx.y;
+    if (c >= a.la_channels) return;
+    const int4 st = J.state[c];
+    const int cur = st.x, act = st.y;
+    if (st.z != 0 || (st.w & (FLAG_INBUF | FLAG_PRE)) || act <= P) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) J.state[c].w = st.w & ~FLAG_GW;
+        return;
+    }
+    const int f = (int)blockIdx.x * 256 + (int)threadIdx.x;  // float4 slot
+    const size_t rows = (size_t)J.S * B;
+    const float4 *H4 = reinterpret_cast<const float4 *>(J.H + (size_t)c * rows) + f;
+    const float4 *X4 = reinterpret_cast<const float4 *>(J.X + (size_t)c * rows) + f;
+    Acc2 w[P];
+    float4 xr[P];  // X at ring offset o (from cur') in xr[o % P]
+#pragma unroll
+    for (int k = 0; k < P; ++k) w[k].zero();
+#pragma unroll
+    for (int o = 1; o < P; ++o) {
+        DBG_CHECK((cur + o) % act < J.S, 41, cur, o, act, J.S);
+        xr[o] = ntld4(X4 + (size_t)((cur + o) % act) * F);
+    }
+    int i0 = P;
+    for (; i0 + P <= act; i0 += P) {  // P rows in flight
+        float4 h[P], xn[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
+            xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int k = 0; k < P; ++k) w[k].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
+#pragma unroll
+        for (int j = 0; j < P; ++j) xr[j] = xn[j];
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        if (i0 + j < act) {
+            const float4 h = ntld4(H4 + (size_t)(i0 + j) * F);
+            xr[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
+#pragma unroll
+            for (int k = 0; k < P; ++k) w[k].mac(h, xr[(j - k + P) % P]);
+        }
+    }
+    float4 *W4 = reinterpret_cast<float4 *>(a.gw + (size_t)c * P * B) + f;
+#pragma unroll
+    for (int k = 0; k < P; ++k) ntst4(W4 + (size_t)k * F, w[k].get(f));
+    if (blockIdx.x == 0 && threadIdx.x == 0) J.state[c].w = st.w | FLAG_GW;
 }
 
 template <int LOG2B, int NT, bool ZZ, bool NTL>
@@ -1729,7 +1836,190 @@ __global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_replay_kernel(Tail0Args 
     if (threadIdx.x == 0) t.err[c] = 0;
 }
 
+// The whole flush in ONE launch at B = 64 (cfg3's head; one slot chunk per
+// channel): per channel workgroup, (1) the pending blocks' R2C by the four
+// waves into the LDS X rows, (2) the MAC of tail0_mac_kernel, (3) each
+// block's C2R, (4) overlap-add, overlap save, the FDL rows and the state --
+// or, if a block's conv slot 0 is not finite, the block-by-block replay of
+// tail0_replay_kernel.  The same arithmetic in the same order as the five
+// kernels (bit-identical); the spectra, convs and C2R outputs stay in LDS.
+// LDS: [H rows + zero | X rows (q >= -1) + zero rows] (the C2R outputs
+// reuse the H rows once the MAC is done) | tw | 4 x 2 B-point FFT buffers |
+// conv rows (the inputs before the MAC) | overlap | flag
+template <int LOG2B>
+__host__ __device__ constexpr size_t tail0_fused_lds(int act, int n) {
+    constexpr size_t B = (size_t)1 << LOG2B;
+    return tail0_mac_lds<LOG2B>(act, n) + 2 * B * 8 + 4 * 2 * B * 8 + (size_t)n * (B / 2) * 16 + B * 4 + 16;
+}
+template <int LOG2B>
+__host__ __device__ constexpr bool tail0_fused_fits(int act, int n) {
+    constexpr size_t B = (size_t)1 << LOG2B;
+    return LOG2B == 6 && n <= (256 / T0_FC) * T0_J && tail0_fused_lds<LOG2B>(act, n) <= 160 * 1024 &&
+           (size_t)(act + 1) * T0_FC * 16 >= (size_t)n * 2 * B * 4;
+}
+template <int LOG2B>
+__global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B, F = B / 2, FC = T0_FC, J = T0_J, RS = J + 1, NT = 256;
+    static_assert(F == FC, "one slot chunk per channel (B = 64)");
+    constexpr float invN = 1.0f / (float)(2 * B);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ProcJob &J0 = t.pa.job[0];
+    const size_t c = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int4 st = J0.state[c];
+    const int cur0 = st.x, act = st.y, n = t.n;
+    const size_t rows = (size_t)J0.S * B;
+    float4 *Hs = reinterpret_cast<float4 *>(smem);   // [act + 1][FC]
+    float4 *Xs = Hs + (size_t)(t.act + 2) * FC;       // Xs[q * FC], q >= -1
+    unsigned char *rest = smem + tail0_mac_lds<LOG2B>(t.act, n);
+    float2 *twl = reinterpret_cast<float2 *>(rest);
+    float2 *wb = twl + 2 * B;                          // [4 waves][2][B]
+    float4 *cvs = reinterpret_cast<float4 *>(wb + 4 * 2 * B);  // [n][F]
+    float *ins = reinterpret_cast<float *>(cvs);       // [n][B] inputs, before the MAC
+    float *ovs = reinterpret_cast<float *>(cvs + (size_t)n * F);
+    int &s_err = *reinterpret_cast<int *>(ovs + B);
+    float *ys = reinterpret_cast<float *>(smem);       // [n][2B], over the H rows after the MAC
+    const bool geo = act == t.act;  // (not the geometry the LDS was sized for: replay)
+
+    // ---- prologue: every row by LDS-DMA (no VGPRs, all in flight) ----
+    const float4 *H = reinterpret_cast<const float4 *>(J0.H + c * rows);
+    const float4 *X = reinterpret_cast<const float4 *>(J0.X + c * rows);
+    const int nq = act - 1 + n;
+    if (tid == 0) s_err = geo ? 0 : 1;
+    if (geo) {
+        for (int idx = tid; idx < FC; idx += NT) Hs[(size_t)act * FC + idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int idx = tid; idx < (J + 1) * FC; idx += NT) {
+            const int q = idx < FC ? -1 : nq + idx / FC - 1;
+            Xs[(size_t)q * FC + idx % FC] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const int half = lane >> 5, f = lane & 31;
+        for (int r2 = wave * 2; r2 < act; r2 += 8)  // IR rows, two per wave instruction
+            if (r2 + half < act)
+                __builtin_amdgcn_global_load_lds((gptr_t)(H + (size_t)(r2 + half) * F + f),
+                                                 (lptr_t)(Hs + (size_t)r2 * FC), 16, 0, 0);
+        for (int r2 = wave * 2; r2 < act - 1; r2 += 8) {  // the previous period's FDL rows
+            const int q = r2 + half;
+            int r = cur0 + act - 1 - q;
+            if (r >= act) r -= act;
+            if (q < act - 1)
+                __builtin_amdgcn_global_load_lds((gptr_t)(X + (size_t)r * F + f), (lptr_t)(Xs + (size_t)r2 * FC), 16,
+                                                 0, 0);
+        }
+        dma_16b<NT>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
+        dma_f32<NT>(ovs, J0.overlap + c * B, B);
+        for (int k = wave; k < n; k += 4)  // (tail_input blocks: the job's input, stride T)
+            dma_f32<64>(ins + (size_t)k * B, J0.in + c * J0.in_stride + (size_t)k * B, B);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (!geo) goto replay;
+    {
+        // ---- (1) R2C of each pending block (:229-241) into its X row ----
+        float2 *bA = wb + (size_t)wave * 2 * B, *bB = bA + B;
+        for (int k = wave; k < n; k += 4) {
+            for (int m = lane; m < B; m += 64)
+                bA[m] = m < B / 2 ? make_float2(ins[(size_t)k * B + 2 * m], ins[(size_t)k * B + 2 * m + 1])
+                                  : make_float2(0.f, 0.f);
+            wave_sync();
+            float2 *Z = lds_cfft<LOG2B, 64, false, true>(bA, bB, twl);
+            float2 *xr = reinterpret_cast<float2 *>(Xs + (size_t)(k + act - 1) * FC);
+            for (int m = lane; m < B; m += 64) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
+            wave_sync();
+        }
+        __syncthreads();
+        // ---- (2) the MAC of tail0_mac_kernel, conv rows to LDS ----
+        const int fl = tid % FC, g = tid / FC, kb0 = g * J;
+        if (kb0 < n) {
+            auto xq = [&](int q) { return Xs[q * FC + fl]; };
+            LaAcc acc[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) acc[j].zero();
+            const bool z0 = fl == 0;
+            const int Q1 = kb0 + act - 2;
+            float4 xr[RS];
+#pragma unroll
+            for (int e = 0; e < J; ++e) xr[e] = xq(Q1 + J - 1 - e);
+            float4 hn = Hs[(size_t)min(1, act) * FC + fl];
+            const int ns = act - 1;
+            for (int s0 = 0; s0 < ns; s0 += RS) {
+#pragma unroll
+                for (int u = 0; u < RS; ++u) {
+                    const int sidx = s0 + u;
+                    if (sidx >= ns) break;
+                    const float4 h = hn;
+                    xr[(u + J) % RS] = xq(Q1 - 1 - sidx);
+                    hn = Hs[(size_t)min(sidx + 2, act) * FC + fl];
+                    const LaH ho = la_ops(h, z0);
+#pragma unroll
+                    for (int j = 0; j < J; ++j) acc[j].mac(ho, xr[(u + J - 1 - j) % RS]);
+                }
+            }
+            const float4 h0 = Hs[fl];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int k = kb0 + j;
+                if (k < n) cvs[(size_t)k * F + fl] = slot_mac(acc[j].get(), Xs[(size_t)(k + act - 1) * FC + fl], h0, fl);
+            }
+        }
+        __syncthreads();
+        // ---- (3) each block's C2R (realfft's error: a non-finite DC / Nyquist) ----
+        for (int k = wave; k < n; k += 4) {
+            const float2 *Zc = reinterpret_cast<const float2 *>(cvs + (size_t)k * F);
+            if (lane == 0 && !(isfinite(Zc[0].x) && isfinite(Zc[0].y))) s_err = 1;
+            for (int m = lane; m < B; m += 64) bA[m] = real_pre<LOG2B, 64>(Zc, m, twl);
+            wave_sync();
+            const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(bA, bB, twl));
+            float *yr = ys + (size_t)k * 2 * B;
+            for (int j = lane; j < 2 * B; j += 64) yr[j] = y[j];
+            wave_sync();
+        }
+        __syncthreads();
+        if (s_err) goto replay;
+        // ---- (4) overlap-add (:270-274), overlap save (:283-284), FDL rows, state ----
+        float *outc = J0.out + c * J0.out_stride;
+        for (int idx = tid; idx < n * B; idx += NT) {
+            const int k = idx >> LOG2B, j = idx & (B - 1);
+            const float ov = k == 0 ? ovs[j] : ys[(size_t)(k - 1) * 2 * B + B + j] * invN;
+            outc[idx] = ys[(size_t)k * 2 * B + j] * invN + ov;
+        }
+        for (int j = tid; j < B; j += NT) J0.overlap[c * B + j] = ys[(size_t)(n - 1) * 2 * B + B + j] * invN;
+        if (st.w & FLAG_INBUF)
+            for (int j = tid; j < B; j += NT) J0.inbuf[c * B + j] = 0.f;
+        float2 *Xc = J0.X + c * rows;
+        const int kf = max(0, n - act);
+        for (int idx = tid; idx < (n - kf) * B; idx += NT) {
+            const int k = kf + (idx >> LOG2B), m = idx & (B - 1);
+            int r = (cur0 - k) % act;
+            if (r < 0) r += act;
+            Xc[(size_t)r * B + m] = reinterpret_cast<const float2 *>(Xs + (size_t)(k + act - 1) * FC)[m];
+        }
+        if (tid == 0) {
+            int cur = (cur0 - n) % act;
+            if (cur < 0) cur += act;
+            const int flags = (st.w & ~(FLAG_PRE | FLAG_INBUF)) ^ ((n & 1) ? FLAG_REV : 0);
+            J0.state[c] = make_int4(cur, act, 0, la_clear(flags, t.pa));
+        }
+        return;
+    }
+replay:
+    // tail_convolver0.process block by block from the untouched state (the
+    // FDL, the overlap and the state word are not written above)
+    for (int k = 0; k < n; ++k) {
+        ProcJob Jk = J0;
+        Jk.in = J0.in + (size_t)k * B;
+        Jk.out = J0.out + (size_t)k * B;
+        Jk.n = B;
+        __syncthreads();  // (the LDS is the generic step's now; the previous block's state word is stored)
+        const int4 sk = J0.state[c];
+        process_job<LOG2B, NT, false, false>(t.pa, Jk, c, sk, smem);
+    }
+}
+
 static int g_variant = VARIANT_AUTO;
+// the scan bits 0-2 (zig-zag, nontemporal, no pipelined step) override the
+// automatic load / step policy only when one of them is set: a variant of
+// feature bits alone (bits 3-10) keeps the automatic policy
+static bool scan_variant_set() { return g_variant != VARIANT_AUTO && (g_variant & 7) != 0; }
 static int g_lag = -1;
 
 // Pipelined step: FDL rows the three stream waves take alone while wave 0
@@ -1756,7 +2046,7 @@ static int pipeline_lag(int) { return g_lag >= 0 ? g_lag : (1 << 30); }
 // fewer loads than four).  It changes the summation order, so it is chosen
 // per channel geometry (never by channel count): shards stay bit-identical.
 static int pick_variant(const ProcArgs &a, int channels, int log2b) {
-    if (g_variant != VARIANT_AUTO) return g_variant;
+    if (scan_variant_set()) return g_variant;
     double stream = 0.0;
     long long rows = 0;
     for (int j = 0; j < a.njobs; ++j) {
@@ -1764,8 +2054,33 @@ static int pick_variant(const ProcArgs &a, int channels, int log2b) {
         rows = std::max(rows, (long long)a.job[j].S);
     }
     const int nt = stream > 192.0 * 1024 * 1024 ? VARIANT_NT : 0;
-    return nt | ((rows << log2b) > 16384 ? VARIANT_NOPIPE : 0);
+    return nt | ((rows << log2b) > 16384 ? VARIANT_NOPIPE : 0) | (g_variant == VARIANT_AUTO ? 0 : g_variant);
 }
+
+template <int LOG2B>
+static hipError_t launch_gw_anchor_t(const ProcArgs &a, int channels, hipStream_t s) {
+    constexpr int F = (1 << LOG2B) / 2;
+    static_assert(F % 256 == 0, "a workgroup covers 256 slots");
+    const int cls = a.gw_t % kGwP;
+    if (channels <= cls || a.gw == nullptr) return hipSuccess;
+    ProcArgs args = a;
+    args.la_channels = channels;
+    const int ny = (channels - cls + kGwP - 1) / kGwP;
+    hipLaunchKernelGGL(gw_anchor_kernel<LOG2B>, dim3(F / 256, ny), dim3(256), 0, s, args);
+    return hipGetLastError();
+}
+
+hipError_t launch_gw_anchor(int log2b, const ProcArgs &a, int channels, hipStream_t s) {
+    switch (log2b) {
+        case 10: return launch_gw_anchor_t<10>(a, channels, s);
+        case 11: return launch_gw_anchor_t<11>(a, channels, s);
+        case 12: return launch_gw_anchor_t<12>(a, channels, s);
+        case 13: return launch_gw_anchor_t<13>(a, channels, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+bool gw_supported(int log2b, int S) { return log2b >= 10 && log2b <= kMaxLog2Fused && S >= 3 * kGwP; }
 
 template <int LOG2B>
 static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t s) {
@@ -1809,6 +2124,18 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
+        }
+        if constexpr (LOG2B == 6) {
+            if (tail0_fused_fits<LOG2B>(a.act, a.n) && !(g_variant != VARIANT_AUTO && (g_variant & VARIANT_T0SPLIT))) {
+                const size_t fl = tail0_fused_lds<LOG2B>(a.act, a.n);
+                auto fk = tail0_fused_kernel<LOG2B>;
+                if (hipError_t e = hipFuncSetAttribute((const void *)fk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)fl);
+                    e != hipSuccess)
+                    return e;
+                hipLaunchKernelGGL(fk, dim3(channels), dim3(256), fl, s, t);
+                return hipGetLastError();
+            }
         }
         hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
         hipLaunchKernelGGL(mk, dim3(channels, F / FC), dim3(256), lds, s, t);
@@ -1954,7 +2281,7 @@ static hipError_t launch_la_t(const ProcArgs &a, int channels, hipStream_t s) {
         // the full-pass streams: nontemporal once the whole H + FDL working
         // set exceeds the Infinity Cache
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
-        const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
+        const bool ntl = !scan_variant_set() ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
         auto kern = a.la_mix == 1   ? (ntl ? upols_la_kernel<LOG2B, true, 1> : upols_la_kernel<LOG2B, false, 1>)
                     : a.la_mix == 2 ? (ntl ? upols_la_kernel<LOG2B, true, 2> : upols_la_kernel<LOG2B, false, 2>)
                     : xf3           ? (ntl ? upols_la_kernel<LOG2B, true, 3> : upols_la_kernel<LOG2B, false, 3>)
@@ -2038,7 +2365,7 @@ static hipError_t launch_rebuild_t(const ProcArgs &a, int channels, hipStream_t 
         constexpr size_t lds = (LG::anchor_bytes + 15) / 16 * 16 + 16;
         if (!a.laW || a.njobs != 1 || a.job[0].n != (1 << LOG2B)) return hipErrorInvalidValue;
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
-        const bool ntl = g_variant == VARIANT_AUTO ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
+        const bool ntl = !scan_variant_set() ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
         auto kern = ntl ? la_rebuild_kernel<LOG2B, true> : la_rebuild_kernel<LOG2B, false>;
         ProcArgs args = a;
         args.la_channels = channels;
@@ -2143,7 +2470,8 @@ hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hip
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 511); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 2047); }
+bool gw_windows_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_NOGW); }
 bool tail0_defer_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_T0BLOCK); }
 bool la_fuse_mix_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_NOFMIX); }
 void set_pipeline_lag(int rows) { g_lag = rows < 0 ? -1 : rows; }

@@ -27,11 +27,15 @@ enum : int {
     // block's C2R failed (the call's output is zero-filled, :264-267); the
     // call's remaining launches skip it, the last one clears the flag
     FLAG_CALLDONE = 1 << 10,
+    // far-row windows of the generic step (B >= 1024, gw_anchor_kernel): the
+    // channel's P windows were anchored after the step of its class and every
+    // step since read one and advanced
+    FLAG_GW = 1 << 11,
     SEQ_SHIFT = 24,
     // lookahead: pre[] holds the near rows' sum (rows D0..1) of the block
     // that starts at `current`, left by the previous step (la.hpp)
     FLAG_NEAR = 1 << 26,
-    LA_MASK = FLAG_LA1 | FLAG_LA2 | FLAG_LA3 | FLAG_NEAR,
+    LA_MASK = FLAG_LA1 | FLAG_LA2 | FLAG_LA3 | FLAG_NEAR | FLAG_GW,
     SEQ_MASK = 3 << SEQ_SHIFT,
 };
 
@@ -42,6 +46,8 @@ enum : int {
     VARIANT_NOFMIX = 64,  // crossfade on the lookahead step: stand-alone mix kernel instead of B's epilogue
     VARIANT_IRBLOCK = 128,  // IR transforms: one segment per workgroup (else one per wave, 64 <= B <= 1024)
     VARIANT_T0BLOCK = 256,  // two-stage: tail0 per block (else deferred to the end of its period), read at create
+    VARIANT_T0SPLIT = 512,  // deferred tail0 at B = 64: the five-kernel flush instead of the fused one (tests)
+    VARIANT_NOGW = 1024,    // B >= 1024: no far-row windows, every step sums its far rows itself (tests)
     VARIANT_AUTO = 0x7fffffff
 };
 void set_variant(int v);
@@ -148,6 +154,13 @@ struct ProcArgs {
     // geometry's tables and the chunks to run (an upper bound over channels)
     LgTab lg;
     int lg_chunks;
+    // far-row windows of the generic step (B >= 1024, gw_anchor_kernel):
+    // gw_p = the split row P (pre = rows 1..P-1 + rows P..act-1; 0 = one sum),
+    // gw = [C][P][B] windows (null: no step of this launch reads one), gw_t =
+    // the batch's one-block step count mod P (channel c reads row (gw_t-1-c) mod P)
+    float2 *gw;
+    int gw_p;
+    int gw_t;
 };
 
 struct IrArgs {
@@ -254,6 +267,15 @@ hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipSt
 // four-step long-block path (large.hip).
 constexpr int kMaxLog2Fused = 13;
 constexpr int kMaxLog2Block = 22;
+// far-row windows (gw_anchor_kernel): window rows per channel = the split row
+constexpr int kGwP = 8;
+// a batch of this geometry sums far rows through windows: 1024 <= B <= 8192
+// and enough far rows to pay for the anchors
+bool gw_supported(int log2b, int S);
+bool gw_windows_allowed();  // VARIANT_NOGW unset
+// the windows of the channels of class a.gw_t mod kGwP, from the state after
+// the step just launched (a.job[0]: H, X, state, S; a.la_channels channels)
+hipError_t launch_gw_anchor(int log2b, const ProcArgs &a, int channels, hipStream_t s);
 // M = 2^log2b = M1 x M2 of the long-block path; bin k of a spectrum row sits
 // at position (k mod M1) * M2 + k / M1
 void lg_split(int log2b, int *l1, int *l2);

@@ -67,6 +67,7 @@ SIGNATURES = {
     "fftconv_uniform_synchronize": (_i, [_vp]),
     "fftconv_uniform_channels": (_sz, [_vp]),
     "fftconv_uniform_lookahead_parts": (_i, [_vp]),
+    "fftconv_uniform_far_windows": (_i, [_vp]),
     "fftconv_uniform_block_size": (_sz, [_vp]),
     "fftconv_uniform_seg_count": (_sz, [_vp]),
     "fftconv_uniform_ir_spectrum": (_i, [_vp, _sz, _sz, _fp]),
@@ -362,6 +363,10 @@ class FFTConvolver(_Base):
     def lookahead_parts(self) -> int:
         """Anchor workgroups per channel of the lookahead step (0 = not used)."""
         return int(lib().fftconv_uniform_lookahead_parts(self._h))
+
+    def far_windows(self) -> int:
+        """Window rows per channel of the far-row windows (B >= 1024; 0 = not used)."""
+        return int(lib().fftconv_uniform_far_windows(self._h))
 
     def ir_spectrum(self, channel: int, segment: int) -> np.ndarray:
         """segments_ir[segment] of a channel: complex64[B + 1]."""

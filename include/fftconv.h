@@ -90,7 +90,8 @@ int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *inp
  * never changes a result bit),
  * else bit 0 = zig-zag segment order on alternate blocks, bit 1 =
  * nontemporal H/X loads, bit 2 = no pipelined step (every call computes
- * its pre_multiplied at block start, as the reference does), bit 3 = no
+ * its pre_multiplied at block start, as the reference does) -- when none
+ * of bits 0-2 is set, the automatic load and step policy stays --, bit 3 = no
  * crossfade pair launch (A and B stream the shared FDL separately), bit 4 =
  * no lookahead step (see below), bit 5 = lookahead launches without anchors
  * (every full block sums all its FDL rows itself; bit-identical to the
@@ -100,7 +101,10 @@ int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *inp
  * transforms (init / update) one segment per workgroup (by default one per
  * wave for 64 <= B <= 1024; bit-identical), bit 8 = two-stage tail0 runs
  * per head block (by default its blocks are convolved together at the end
- * of each tail period; read when a TwoStageFFTConvolver is created).
+ * of each tail period; read when a TwoStageFFTConvolver is created), bit 9 =
+ * that end-of-period flush in five kernels instead of one (head block 64;
+ * bit-identical), bit 10 = no far-row windows for 1024 <= B <= 8192 (every
+ * one-block call sums its far rows itself; bit-identical).
  * Lookahead (automatic for standalone FFTConvolver batches with
  * 128 <= B <= 512 and >= 40 segments, full-block calls from an empty input
  * buffer): the FDL sum of each block is re-associated in time over a near
@@ -183,6 +187,11 @@ int fftconv_uniform_synchronize(fftconv_uniform *h);
 size_t fftconv_uniform_channels(const fftconv_uniform *h);
 /* anchor workgroups per channel of the lookahead step, 0 = not used */
 int fftconv_uniform_lookahead_parts(const fftconv_uniform *h);
+/* window rows per channel of the generic step's far-row windows (automatic
+ * for standalone batches with 1024 <= B <= 8192 and >= 24 segments: an
+ * anchor every P blocks sums rows >= P for a channel's next P one-block
+ * calls; bit-identical to summing them every block), 0 = not used */
+int fftconv_uniform_far_windows(const fftconv_uniform *h);
 size_t fftconv_uniform_block_size(const fftconv_uniform *h);   /* next_power_of_two(max_block_size) */
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h);
 /* segments_ir[segment] of one channel (src/fft_convolver.rs:92): B+1 bins,

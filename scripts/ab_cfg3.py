@@ -2,6 +2,7 @@
 """Same-process, interleaved A/B of several builds of libfftconv_amd.so on the
 cfg3 workload (TwoStageFFTConvolver, head 64 / tail 4096, IR 262144, 256
 channels; one process_device_steps call per tail period of 64 head calls).
+Each LIB may carry knobs applied before its timed runs: PATH,variant=1024.
 usage: ab_cfg3.py LIB1 LIB2 ... [--rounds R] [--periods P]"""
 import argparse
 import ctypes as C
@@ -34,7 +35,10 @@ irs = shard.synth_irs(range(Cn), L)
 x = torch.from_numpy(shard.synth_dry(range(Cn), steps, B)).cuda()  # [steps][C][B]
 handles = []
 loaded = {}
-for path in a.libs:
+knobs = []
+for spec in a.libs:
+    path, *kv = spec.split(",")
+    knobs.append(dict(k.split("=") for k in kv))
     if path not in loaded:
         loaded[path] = C.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
     lib = loaded[path]
@@ -45,7 +49,7 @@ for path in a.libs:
                                                           C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p]
     h = lib.fftconv_twostage_init_batch(0, Cn, irs.ctypes.data, L, L, B, L)
     assert h, path
-    handles.append((lib, h, torch.empty((steps, Cn, B), device="cuda")))
+    handles.append((lib, h, torch.empty((steps, Cn, B), device="cuda"), int(knobs[-1].get("variant", -1))))
 del irs
 
 
@@ -58,7 +62,8 @@ def period(lib, h, y):
 res = [[] for _ in handles]
 host = [[] for _ in handles]
 for r in range(a.rounds):
-    for idx, (lib, h, y) in enumerate(handles):
+    for idx, (lib, h, y, var) in enumerate(handles):
+        lib.fftconv_set_kernel_variant(var)
         period(lib, h, y)  # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
@@ -76,3 +81,6 @@ for path, r, hr in zip(a.libs, res, host):
     print(f"{path}: median {us:.3f} us/step (min {min(r):.3f}) -> {Cn * B / us:.1f} MS/s; "
           f"host enqueue {statistics.median(hr):.3f} us/step")
 print("outputs bit-identical across builds:", same)
+for lib, h, _, _ in handles:  # (destroyed before exit: no live handle at library teardown)
+    lib.fftconv_twostage_destroy.argtypes = [C.c_void_p]
+    lib.fftconv_twostage_destroy(h)

@@ -125,3 +125,47 @@ def test_per_block_tail0_path(amd, oracle_mod):
     got = np.concatenate([conv.process(white(np.random.default_rng(k), n)) for k, n in enumerate(chunks)])
     exp = np.concatenate([ref.process(white(np.random.default_rng(k), n)) for k, n in enumerate(chunks)])
     assert_close(got, exp, what="per-block tail0")
+
+
+T0SPLIT = 512  # VARIANT_T0SPLIT: the five-kernel flush instead of the fused one (read per launch)
+
+
+def test_fused_flush_bitwise_equals_split(amd, oracle_mod):
+    """The fused end-of-period flush (tail0_fused_kernel, head block 64) and
+    the five-kernel flush run the same arithmetic in the same order:
+    bit-identical outputs, through a NaN block's replay on one channel, and
+    both against the oracle."""
+    head, L, C = 64, 12000, 3
+    hs = np.stack([ir(np.random.default_rng(20 + c), L) for c in range(C)])
+    outs = []
+    for v in (-1, T0SPLIT):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.TwoStageFFTConvolver.init(hs, head, L, channels=C)
+            T = conv.tail_block_size
+            per = T // head
+            rng = np.random.default_rng(21)
+            ys = []
+            for j in range(3 * per + 5):
+                x = np.stack([white(rng, head) for _ in range(C)])
+                if j == per + 4:
+                    x[1, 9] = np.nan
+                ys.append(conv.process(x))
+            outs.append(np.concatenate(ys, axis=1))
+        finally:
+            amd.set_kernel_variant(-1)
+    assert np.array_equal(outs[0], outs[1], equal_nan=True)
+    rng = np.random.default_rng(21)
+    refs = [oracle_mod.TwoStageFFTConvolver.init(hs[c], head, L) for c in range(C)]
+    exp = [[] for _ in range(C)]
+    for j in range(3 * per + 5):
+        x = np.stack([white(rng, head) for _ in range(C)])
+        if j == per + 4:
+            x[1, 9] = np.nan
+        for c in range(C):
+            exp[c].append(refs[c].process(x[c]))
+    for c in range(C):
+        e = np.concatenate(exp[c])
+        assert np.array_equal(np.isnan(outs[0][c]), np.isnan(e))
+        m = ~np.isnan(e)
+        assert_close(outs[0][c][m], e[m], what=f"channel {c}")

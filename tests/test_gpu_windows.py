@@ -1,0 +1,145 @@
+"""Far-row windows of the generic step (1024 <= B <= 8192, >= 24 segments;
+csrc/kernels.hip gw_anchor_kernel).
+
+FFTConvolver::process (src/fft_convolver.rs:215-295) with the FDL sum of a
+one-block call split as rows 1..P-1 (summed by the step) plus rows P..act-1
+(summed by an anchor every P calls for the channel's next P blocks).  Checked
+against the oracle (tolerance REL_TOL, as every parity test) and for the
+property the design rests on: the split is canonical, so the bits do not
+depend on whether a step read a window (VARIANT_NOGW), the channel's anchor
+class, its shard, a clone, or the call pattern around it."""
+import numpy as np
+import pytest
+
+from common import assert_close, ir, white
+
+pytestmark = pytest.mark.gpu
+
+NOGW = 1024
+
+
+def _refs(oracle_mod, hs, B, L):
+    return [oracle_mod.FFTConvolver.init(hs[c], B, L) for c in range(hs.shape[0])]
+
+
+@pytest.mark.parametrize("B,S", [(1024, 30), (2048, 26), (4096, 40), (8192, 25)])
+def test_windows_vs_oracle(amd, oracle_mod, B, S):
+    """Entry, the ring wrapping, partial and multi-block calls, a batch update
+    that shrinks act (ring index mod act), a channel update, a reset."""
+    rng = np.random.default_rng(700 + B)
+    C, L = 11, S * B - 5
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    assert conv.far_windows() == 8
+    refs = _refs(oracle_mod, hs, B, L)
+    chunks = [B] * (S + 12) + [B // 3, B - B // 3] + [B] * 11 + [2 * B] + [B] * 13 + [B // 2] + [B] * 9
+    for j, k in enumerate(chunks):
+        if j == S + 4:
+            hn = np.stack([ir(rng, L - 3 * B) for _ in range(C)])
+            conv.update(hn)
+            for c in range(C):
+                refs[c].update(hn[c])
+        if j == S + 30:
+            hn = ir(rng, L)
+            conv.update_channel(9, hn)
+            refs[9].update(hn)
+        x = np.stack([white(rng, k) for _ in range(C)])
+        got = conv.process(x)
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"B={B} chunk {j} ch {c}")
+    for c in range(C):
+        assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
+    conv.reset()
+    for c in range(C):
+        refs[c].reset()
+    for j in range(12):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        got = conv.process(x)
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"after reset, block {j}")
+
+
+def test_windows_equal_full_sum(amd):
+    """Steps served from windows give the same bits as steps that sum their
+    far rows themselves (VARIANT_NOGW), through a partial call and re-entry."""
+    rng = np.random.default_rng(710)
+    C, B, L = 13, 1024, 33 * 1024 + 7
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    ks = [B] * 40 + [300, B - 300] + [B] * 25 + [3 * B] + [B] * 10
+    xs = [np.stack([white(rng, k) for _ in range(C)]) for k in ks]
+    outs = {}
+    for v in (-1, NOGW):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+            outs[v] = np.concatenate([conv.process(x) for x in xs], axis=1)
+        finally:
+            amd.set_kernel_variant(-1)
+    assert np.array_equal(outs[-1], outs[NOGW])
+
+
+def test_windows_class_independent(amd):
+    """11 identical channels in 8 anchor classes: bit-identical outputs."""
+    rng = np.random.default_rng(720)
+    C, B, L = 11, 2048, 30 * 2048
+    h = ir(rng, L)
+    conv = amd.FFTConvolver.init(np.tile(h, (C, 1)), B, L, channels=C)
+    for j in range(50):
+        y = conv.process(np.tile(white(rng, B), (C, 1)))
+        for c in range(1, C):
+            assert np.array_equal(y[c], y[0]), (j, c)
+
+
+def test_windows_shards_and_clone(amd):
+    """A 12-channel batch split 5 + 7 (every channel changes class and index)
+    stays bit-identical; a clone taken mid-window continues bit-identically."""
+    rng = np.random.default_rng(730)
+    C, B, L = 12, 1024, 28 * 1024
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    one = amd.FFTConvolver.init(hs, B, L, channels=C)
+    a = amd.FFTConvolver.init(hs[:5], B, L, channels=5)
+    b = amd.FFTConvolver.init(hs[5:], B, L, channels=7)
+    for j in range(45):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        assert np.array_equal(one.process(x), np.concatenate([a.process(x[:5]), b.process(x[5:])])), j
+    twin = one.clone()
+    for j in range(20):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        assert np.array_equal(one.process(x), twin.process(x)), j
+
+
+def test_windows_nan_block(amd, oracle_mod):
+    """A non-finite block in one channel while its neighbours read windows:
+    zero output, block kept in the input buffer, then recovery (the channel
+    re-anchors) -- as the oracle."""
+    rng = np.random.default_rng(740)
+    C, B, L = 9, 1024, 30 * 1024
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    refs = _refs(oracle_mod, hs, B, L)
+    for j in range(60):
+        x = np.stack([white(rng, B) for _ in range(C)])
+        if j in (35, 36):
+            x[6, 17] = np.nan
+        got = conv.process(x)
+        for c in range(C):
+            r = refs[c].process(x[c])
+            assert np.array_equal(np.isnan(got[c]), np.isnan(r)), (j, c)
+            m = ~np.isnan(r)
+            assert_close(got[c][m], r[m], what=f"block {j} ch {c}")
+            assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
+
+
+def test_windows_twostage_tail(amd, oracle_mod):
+    """The two-stage tail (head 32: T = 1024 with 32 segments) runs on
+    windows: the output is the oracle's over 12 tail periods."""
+    rng = np.random.default_rng(750)
+    head, L = 32, 34000
+    h = ir(rng, L)
+    conv = amd.TwoStageFFTConvolver.init(h, head, L)
+    ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
+    T = conv.tail_block_size
+    assert T == 1024 and ref.tail_block_size == T
+    for j in range(12 * T // head):
+        x = white(rng, head)
+        assert_close(conv.process(x), ref.process(x), what=f"call {j}")
