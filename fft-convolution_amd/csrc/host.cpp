@@ -896,7 +896,10 @@ struct TwoStageCore {
             tail.reset(new (std::nothrow) UniformCore());
             if (!tail) return fail(FFTCONV_E_NOMEM, "out of host memory");
             tail->parent_stream = stream;
-            tail->gw_ok = true;  // one full-block call per period: far-row windows
+            // one full-block call per period: far-row windows (tuning, read at
+            // creation: FFTCONV_TAIL_GW=0 turns them off)
+            const char *gwe = getenv("FFTCONV_TAIL_GW");
+            tail->gw_ok = !gwe || atoi(gwe) != 0;
             st = slice(2 * T, tl, tmp);
             if (int r = tail->init(dev, C, tmp.data(), tl, st, T, tl)) return r;
         }
@@ -907,6 +910,8 @@ struct TwoStageCore {
 
     // fill reached T (:464-491): swap the tail0 buffers, swap the tail buffers,
     // and start the tail convolution of this period on the side stream.
+    // (Starting the tail before the flush, beside it, was slower: 8.17 vs
+    // 7.62 us per cfg3 step, profiles/r4/r4u_ab_cfg3_tail_early_rejected.log.)
     int end_of_period(hipStream_t s) {
         if (int r = flush_t0(s)) return r;  // (tail_output0 is complete before the swap)
         std::swap(tail_precalculated0, tail_output0);                         // :473-475

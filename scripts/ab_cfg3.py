@@ -2,7 +2,8 @@
 """Same-process, interleaved A/B of several builds of libfftconv_amd.so on the
 cfg3 workload (TwoStageFFTConvolver, head 64 / tail 4096, IR 262144, 256
 channels; one process_device_steps call per tail period of 64 head calls).
-Each LIB may carry knobs applied before its timed runs: PATH,variant=1024.
+Each LIB may carry knobs applied before its timed runs: PATH,variant=1024, and
+environment knobs read when its handle is created: PATH,FFTCONV_TAIL_LATE=1.
 usage: ab_cfg3.py LIB1 LIB2 ... [--rounds R] [--periods P]"""
 import argparse
 import ctypes as C
@@ -47,7 +48,13 @@ for spec in a.libs:
                                                 C.c_size_t]
     lib.fftconv_twostage_process_device_steps.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p,
                                                           C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p]
+    for k, v in knobs[-1].items():  # (env knobs, read at creation: FFTCONV_TAIL_LATE=1 ...)
+        if k.startswith("FFTCONV_"):
+            os.environ[k] = v
     h = lib.fftconv_twostage_init_batch(0, Cn, irs.ctypes.data, L, L, B, L)
+    for k in knobs[-1]:
+        if k.startswith("FFTCONV_"):
+            del os.environ[k]
     assert h, path
     handles.append((lib, h, torch.empty((steps, Cn, B), device="cuda"), int(knobs[-1].get("variant", -1))))
 del irs

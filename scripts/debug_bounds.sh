@@ -11,7 +11,7 @@ export FFTCONV_AMD_LIB="$ROOT/fft-convolution_amd/libfftconv_amd_dbg.so"
 export UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"
 out=gpurun_out/debug_bounds.log
 timeout -k 10 900 python -u -m pytest tests/test_gpu_lookahead.py tests/test_gpu_twostage_defer.py \
-    tests/test_gpu_crossfade_twostage.py tests/test_gpu_large.py tests/test_gpu_fullsize.py -v \
+    tests/test_gpu_crossfade_twostage.py tests/test_gpu_large.py tests/test_gpu_fullsize.py tests/test_gpu_windows.py -v \
     --timeout 600 --timeout-method thread -s > "$out" 2>&1
 rc=$?
 echo "pytest rc=$rc"
