@@ -773,36 +773,46 @@ struct TwoStageCore {
         return FFTCONV_OK;
     }
 
-    // The side stream is confined to the first ncu/k CUs (k = the tail's
-    // share of the bytes, 3 at cfg3; the r1 sweep over k = 1..6 is in
-    // profiles/r1/cfg3_tail_cu_div*.log): a T-block tail workgroup fills a whole
-    // CU (1024 lanes x 128 VGPRs), and unconfined it locks the
-    // latency-critical head steps out of the chip for its whole duration
-    // (measured: a 197 us head step behind a 193 us tail).  Contiguous masks
-    // only: power-of-two strided masks read back fine but did not constrain
-    // dispatch (scripts/cumask_probe.hip).  k = 1 disables the mask.
+    // The side stream is confined to the first CUs of the chip, a whole
+    // number of XCDs (32 CUs each, numbered XCD-major): as many as the tail's
+    // share of the bytes streamed per tail period, at least one.  A T-block
+    // tail workgroup fills a whole CU (1024 lanes x 128 VGPRs), and unconfined
+    // it locks the latency-critical head steps out of the chip for its whole
+    // duration (measured: a 197 us head step behind a 193 us tail).  With the
+    // tail's far-row windows cfg3's tail fits one XCD: the head
+    // steps keep the other seven XCDs and their L2s to themselves (6.92 us per
+    // step, vs 7.29 on 36 CUs, 7.23 on 64, 7.54 on 85, and the tail no longer
+    // fits a period on 25 or fewer: profiles/r4/r4w_*, r4x_*).  Contiguous
+    // masks only: power-of-two strided masks read back fine but did not
+    // constrain dispatch (scripts/cumask_probe.hip).
     int create_side_stream() {
-        // default share: the tail's fraction of the bytes streamed per tail
-        // period (cfg3: 4.06 MB of 12.5 MB per channel -> k = 3)
-        int k = 1;
-        if (tail) {
-            const double tail_b = (double)tail->S * (double)tail->B;
-            double per_b = tail_b + (double)(T / std::max<size_t>(head_bs, 1)) *
-                                        (double)((head ? head->S * head->B : 0) + (tail0 ? tail0->S * tail0->B : 0));
-            k = (int)std::lround(per_b / std::max(tail_b, 1.0));
-            k = std::min(8, std::max(2, k));
-        }
-        // (tuning, read once per handle at creation: FFTCONV_TAIL_CU_DIV=k
-        // overrides the share, 1 = unmasked)
-        if (const char *e = getenv("FFTCONV_TAIL_CU_DIV")) k = std::max(1, atoi(e));
         int ncu = 0;
         HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-        if (k <= 1 || ncu <= 0) {
+        int cus = 0;  // 0 = unmasked
+        if (tail && ncu >= 8) {
+            // bytes per tail period in B-bin rows: the tail's step (with windows:
+            // P-1 near rows of H and X, one window row, and 1/P of an anchor's
+            // S H rows, S X rows and P window rows) against T/h head steps
+            const double P = tail->gw_p;
+            const double tail_rows = P > 0 ? (2 * (P - 1) + 1 + (2 * tail->S + P) / P) / 2 : (double)tail->S;
+            const double tail_b = tail_rows * (double)tail->B;
+            const double per_b = tail_b + (double)(T / std::max<size_t>(head_bs, 1)) *
+                                              (double)((head ? head->S * head->B : 0) + (tail0 ? tail0->S * tail0->B : 0));
+            const int nx = std::min(7, std::max(1, (int)std::lround(8.0 * tail_b / std::max(per_b, 1.0))));
+            cus = nx * (ncu / 8);
+        }
+        // (tuning, read once per handle at creation: FFTCONV_TAIL_CU_DIV=k
+        // confines the tail to ncu/k CUs instead, 1 = unmasked)
+        if (const char *e = getenv("FFTCONV_TAIL_CU_DIV")) {
+            const int k = std::max(1, atoi(e));
+            cus = k <= 1 ? 0 : std::max(1, ncu / k);
+        }
+        if (cus <= 0 || cus >= ncu) {
             HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
             return FFTCONV_OK;
         }
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int cu = 0; cu < std::max(1, ncu / k); ++cu) mask[cu / 32] |= 1u << (cu % 32);
+        for (int cu = 0; cu < cus; ++cu) mask[cu / 32] |= 1u << (cu % 32);
         HIP_TRY(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
         return FFTCONV_OK;
     }

@@ -2126,7 +2126,9 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
             if (e != hipSuccess) return e;
         }
         if constexpr (LOG2B == 6) {
-            if (tail0_fused_fits<LOG2B>(a.act, a.n) && !(g_variant != VARIANT_AUTO && (g_variant & VARIANT_T0SPLIT))) {
+            // (opt-in: one kernel flushes faster alone, 46 vs 55 us, but the
+            // cfg3 step beside the tail is slower, 7.54 vs 7.17 us, r4v A/B)
+            if (tail0_fused_fits<LOG2B>(a.act, a.n) && g_variant != VARIANT_AUTO && (g_variant & VARIANT_T0FUSED)) {
                 const size_t fl = tail0_fused_lds<LOG2B>(a.act, a.n);
                 auto fk = tail0_fused_kernel<LOG2B>;
                 if (hipError_t e = hipFuncSetAttribute((const void *)fk, hipFuncAttributeMaxDynamicSharedMemorySize,

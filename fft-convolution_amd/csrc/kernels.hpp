@@ -46,7 +46,7 @@ enum : int {
     VARIANT_NOFMIX = 64,  // crossfade on the lookahead step: stand-alone mix kernel instead of B's epilogue
     VARIANT_IRBLOCK = 128,  // IR transforms: one segment per workgroup (else one per wave, 64 <= B <= 1024)
     VARIANT_T0BLOCK = 256,  // two-stage: tail0 per block (else deferred to the end of its period), read at create
-    VARIANT_T0SPLIT = 512,  // deferred tail0 at B = 64: the five-kernel flush instead of the fused one (tests)
+    VARIANT_T0FUSED = 512,  // deferred tail0 at B = 64: one fused flush kernel instead of five (bit-identical)
     VARIANT_NOGW = 1024,    // B >= 1024: no far-row windows, every step sums its far rows itself (tests)
     VARIANT_AUTO = 0x7fffffff
 };

@@ -102,8 +102,8 @@ int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *inp
  * wave for 64 <= B <= 1024; bit-identical), bit 8 = two-stage tail0 runs
  * per head block (by default its blocks are convolved together at the end
  * of each tail period; read when a TwoStageFFTConvolver is created), bit 9 =
- * that end-of-period flush in five kernels instead of one (head block 64;
- * bit-identical), bit 10 = no far-row windows for 1024 <= B <= 8192 (every
+ * that end-of-period flush in one fused kernel instead of five (head block
+ * 64; bit-identical), bit 10 = no far-row windows for 1024 <= B <= 8192 (every
  * one-block call sums its far rows itself; bit-identical).
  * Lookahead (automatic for standalone FFTConvolver batches with
  * 128 <= B <= 512 and >= 40 segments, full-block calls from an empty input

@@ -127,18 +127,18 @@ def test_per_block_tail0_path(amd, oracle_mod):
     assert_close(got, exp, what="per-block tail0")
 
 
-T0SPLIT = 512  # VARIANT_T0SPLIT: the five-kernel flush instead of the fused one (read per launch)
+T0FUSED = 512  # VARIANT_T0FUSED: one fused flush kernel instead of five (read per launch)
 
 
 def test_fused_flush_bitwise_equals_split(amd, oracle_mod):
-    """The fused end-of-period flush (tail0_fused_kernel, head block 64) and
-    the five-kernel flush run the same arithmetic in the same order:
+    """The five-kernel end-of-period flush (the default) and the fused one
+    (tail0_fused_kernel, head block 64, VARIANT_T0FUSED) run the same arithmetic in the same order:
     bit-identical outputs, through a NaN block's replay on one channel, and
     both against the oracle."""
     head, L, C = 64, 12000, 3
     hs = np.stack([ir(np.random.default_rng(20 + c), L) for c in range(C)])
     outs = []
-    for v in (-1, T0SPLIT):
+    for v in (-1, T0FUSED):
         amd.set_kernel_variant(v)
         try:
             conv = amd.TwoStageFFTConvolver.init(hs, head, L, channels=C)
