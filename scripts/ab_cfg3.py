@@ -2,7 +2,7 @@
 """Same-process, interleaved A/B of several builds of libfftconv_amd.so on the
 cfg3 workload (TwoStageFFTConvolver, head 64 / tail 4096, IR 262144, 256
 channels; one process_device_steps call per tail period of 64 head calls).
-Each LIB may carry knobs applied before its timed runs: PATH,variant=1024, and
+Each LIB may carry knobs applied before its timed runs: PATH,variant=1024,lag=8, and
 environment knobs read when its handle is created: PATH,FFTCONV_TAIL_LATE=1.
 usage: ab_cfg3.py LIB1 LIB2 ... [--rounds R] [--periods P]"""
 import argparse
@@ -56,7 +56,8 @@ for spec in a.libs:
         if k.startswith("FFTCONV_"):
             del os.environ[k]
     assert h, path
-    handles.append((lib, h, torch.empty((steps, Cn, B), device="cuda"), int(knobs[-1].get("variant", -1))))
+    handles.append((lib, h, torch.empty((steps, Cn, B), device="cuda"), int(knobs[-1].get("variant", -1)),
+                    int(knobs[-1].get("lag", -1))))
 del irs
 
 
@@ -69,8 +70,10 @@ def period(lib, h, y):
 res = [[] for _ in handles]
 host = [[] for _ in handles]
 for r in range(a.rounds):
-    for idx, (lib, h, y, var) in enumerate(handles):
+    for idx, (lib, h, y, var, lag) in enumerate(handles):
         lib.fftconv_set_kernel_variant(var)
+        if hasattr(lib, "fftconv_set_pipeline_lag"):
+            lib.fftconv_set_pipeline_lag(lag)
         period(lib, h, y)  # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
@@ -88,6 +91,6 @@ for path, r, hr in zip(a.libs, res, host):
     print(f"{path}: median {us:.3f} us/step (min {min(r):.3f}) -> {Cn * B / us:.1f} MS/s; "
           f"host enqueue {statistics.median(hr):.3f} us/step")
 print("outputs bit-identical across builds:", same)
-for lib, h, _, _ in handles:  # (destroyed before exit: no live handle at library teardown)
+for lib, h, *_ in handles:  # (destroyed before exit: no live handle at library teardown)
     lib.fftconv_twostage_destroy.argtypes = [C.c_void_p]
     lib.fftconv_twostage_destroy(h)
