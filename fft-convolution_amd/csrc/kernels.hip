@@ -494,8 +494,10 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     float ovr[CNB], p0r[CNB], p1r[CNB];
 #pragma unroll
     for (int i = 0; i < CNB; ++i) ovr[i] = p0r[i] = p1r[i] = 0.f;
+    float2 *Z = bufA, *Q = bufB;  // (the chain's transform buffers, across B1)
+    bool err = false;
     if (wave == 0) {
-        // ---- critical chain, one wave ----
+        // ---- critical chain, one wave: R2C, conv, the C2R error check ----
         dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);   // x[0..B) as packed z[0..B/2)
         for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
         dma_16b<64>(twl, a.tw, 2 * B * (int)sizeof(float2));
@@ -524,8 +526,8 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             for (int j = lane; j < B; j += 64) ti[j] = xb[j];
         }
         wave_sync();
-        float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
-        float2 *Q = Z == bufA ? bufB : bufA;
+        Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
+        Q = Z == bufA ? bufB : bufA;
         float2 *Xcur = Xc + (size_t)cur * B;
         for (int m = lane; m < B; m += 64) {
             const float2 v = real_post<LOG2B, 64>(Z, m, twl);
@@ -551,7 +553,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
                 if (f < F) acc[s].mac(reinterpret_cast<const float4 *>(h1l)[f], reinterpret_cast<const float4 *>(Q)[f]);
             }
         }
-        const bool err = __ballot(bad) != 0ull;
+        err = __ballot(bad) != 0ull;
         if constexpr (Gm::PIPE_EARLY) {
             // the chain's share of the next block's pre (row 1, and the last
             // w0 rows with a pipeline lag) to the reduction slots; the helper
@@ -562,8 +564,22 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
 #pragma unroll
             for (int s = 0; s < SPL; ++s) red[s * 64 + lane] = acc[s].get(f0 + s * 64);
             if (lane == 0) s_err = err ? 1 : 0;
-            __syncthreads();  // (B1, the helpers' barrier below)
         }
+    } else if constexpr (Gm::PIPE_EARLY) {
+        // ---- helper waves: FDL rows 2..act-1 - w0 of the next block's pre ----
+        const int R = act > 2 ? act - 2 : 0;
+        const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
+        mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R - w0, NSW, wave - 1, rsub, f0);
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) red[(wave * SPL + s) * 64 + lane] = acc[s].get(f0 + s * 64);
+        proc_stamp(a, 2);
+    }
+    // B1 (B <= 256): every wave at this one barrier -- the chain's share of
+    // the next block's pre and its error flag, and the helpers' shares, are
+    // in the reduction slots
+    if constexpr (Gm::PIPE_EARLY) __syncthreads();
+    if (wave == 0) {
+        // ---- the chain's C2R and overlap-add ----
         wave_sync();
         proc_stamp(a, 1);
         if (!err) {
@@ -603,16 +619,8 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         if constexpr (Gm::PIPE_EARLY) return;
     }
     if constexpr (Gm::PIPE_EARLY) {
-        // ---- helper waves: FDL rows 2..act-1 - w0 of the next block's pre,
-        // then (B1: the chain's share is in the slots) its fixed-order
-        // reduction and the state, while the chain runs its C2R ----
-        const int R = act > 2 ? act - 2 : 0;
-        const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
-        mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R - w0, NSW, wave - 1, rsub, f0);
-#pragma unroll
-        for (int s = 0; s < SPL; ++s) red[(wave * SPL + s) * 64 + lane] = acc[s].get(f0 + s * 64);
-        proc_stamp(a, 2);
-        __syncthreads();  // (B1)
+        // ---- helper waves: the next block's pre in its fixed-order
+        // reduction, and the state, while the chain runs its C2R ----
         const int ht = tid - 64;
         if (s_err) {
             if (ht == 0) J.state[c] = make_int4(cur, act, 0, la_clear(flags | FLAG_INBUF, a));
