@@ -773,14 +773,15 @@ struct TwoStageCore {
         return FFTCONV_OK;
     }
 
-    // The side stream is confined to the first CUs of the chip, a whole
-    // number of XCDs (32 CUs each, numbered XCD-major): as many as the tail's
-    // share of the bytes streamed per tail period, at least one.  A T-block
+    // The side stream is confined to the first CUs of the mask, in units of
+    // ncu/8 (one XCD's worth of CUs; how the mask's CU numbering maps onto
+    // XCDs is not documented): as many units as the tail's share of the
+    // bytes streamed per tail period, at least one.  A T-block
     // tail workgroup fills a whole CU (1024 lanes x 128 VGPRs), and unconfined
     // it locks the latency-critical head steps out of the chip for its whole
     // duration (measured: a 197 us head step behind a 193 us tail).  With the
-    // tail's far-row windows cfg3's tail fits one XCD: the head
-    // steps keep the other seven XCDs and their L2s to themselves (6.92 us per
+    // tail's far-row windows cfg3's tail fits one unit (32 CUs):
+    // the head steps keep the rest of the chip (6.92 us per
     // step, vs 7.29 on 36 CUs, 7.23 on 64, 7.54 on 85, and the tail no longer
     // fits a period on 25 or fewer: profiles/r4/r4w_*, r4x_*).  Contiguous
     // masks only: power-of-two strided masks read back fine but did not
