@@ -1015,7 +1015,7 @@ __global__ __launch_bounds__(256) void gw_anchor_kernel(ProcArgs a) {
 }
 
 template <int LOG2B, int NT, bool ZZ, bool NTL>
-__global__ __launch_bounds__(NT, 4) void upols_process_kernel(ProcArgs a) {
+__global__ __launch_bounds__(NT, NT == 512 ? 2 : 4) void upols_process_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const size_t c = blockIdx.x;
     const ProcJob &J = a.job[blockIdx.y];
@@ -1606,7 +1606,11 @@ constexpr int kNT = 256;
 
 // threads per workgroup of the fused kernel: 256 up to B = 1024; larger
 // blocks get more lanes so each owns <= 4 slots (no spills at 4 waves/SIMD)
-constexpr int proc_nt(int log2b) { return log2b <= 10 ? 256 : (log2b == 11 ? 512 : 1024); }
+// (B >= 2048 on 512 threads at 2 waves per SIMD: B 4096 197 VGPRs, no
+// spills -- on 1024 threads the 128-VGPR cap spilled 34 (B 8192: 96).  A
+// one-block step at 256 channels: B 2048 73.1 -> 70.3 us, B 4096 99.8 ->
+// 92.2 us, B 8192 125.9 -> 117.5 us; bit-identical; r4e / r4f A/Bs)
+constexpr int proc_nt(int log2b) { return log2b <= 10 ? 256 : 512; }
 
 // ---------------------------------------------------------------------------
 // Two-stage tail0 deferred to the end of its period (Tail0Args, kernels.hpp).
