@@ -130,16 +130,42 @@ def test_windows_nan_block(amd, oracle_mod):
             assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
 
 
-def test_windows_twostage_tail(amd, oracle_mod):
-    """The two-stage tail (head 32: T = 1024 with 32 segments) runs on
-    windows: the output is the oracle's over 12 tail periods."""
-    rng = np.random.default_rng(750)
-    head, L = 32, 34000
+@pytest.mark.parametrize("head,L,T", [(32, 34000, 1024), (64, 70000, 2048)])
+def test_windows_twostage_tail(amd, oracle_mod, head, L, T):
+    """The two-stage tail (T = 1024 with 32 segments, T = 2048 with 33) runs
+    on windows: the output is the oracle's over 10 tail periods."""
+    rng = np.random.default_rng(750 + head)
     h = ir(rng, L)
     conv = amd.TwoStageFFTConvolver.init(h, head, L)
     ref = oracle_mod.TwoStageFFTConvolver.init(h, head, L)
-    T = conv.tail_block_size
-    assert T == 1024 and ref.tail_block_size == T
-    for j in range(12 * T // head):
+    assert conv.tail_block_size == T and ref.tail_block_size == T
+    for j in range(10 * T // head):
         x = white(rng, head)
         assert_close(conv.process(x), ref.process(x), what=f"call {j}")
+
+
+def test_windows_device_steps(amd, oracle_mod):
+    """process_device_steps over one-block calls with windows equals host
+    calls bitwise and the oracle on sampled channels."""
+    import torch
+
+    rng = np.random.default_rng(760)
+    C, B, L, K = 9, 1024, 30 * 1024, 40
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    x = np.stack([white(rng, K * B) for _ in range(C)])
+    dev = torch.device("cuda:0")
+    xd = torch.from_numpy(np.ascontiguousarray(x.reshape(C, K, B).transpose(1, 0, 2))).to(dev)  # [K][C][B]
+    yd = torch.empty_like(xd)
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    assert conv.far_windows() == 8
+    s = torch.cuda.Stream(dev)
+    conv.process_device_steps(xd.data_ptr(), B, C * B, yd.data_ptr(), B, C * B, B, K, s.cuda_stream)
+    s.synchronize()
+    y = yd.cpu().numpy().transpose(1, 0, 2).reshape(C, K * B)
+    host = amd.FFTConvolver.init(hs, B, L, channels=C)
+    yh = np.concatenate([host.process(x[:, k * B:(k + 1) * B]) for k in range(K)], axis=1)
+    assert np.array_equal(y, yh)
+    for c in (0, 8):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        assert_close(y[c], np.concatenate([ref.process(x[c, k * B:(k + 1) * B]) for k in range(K)]),
+                     what=f"channel {c}")
