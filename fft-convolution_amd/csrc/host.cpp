@@ -777,7 +777,7 @@ struct TwoStageCore {
     // ncu/8 (one XCD's worth of CUs; how the mask's CU numbering maps onto
     // XCDs is not documented): as many units as the tail's share of the
     // bytes streamed per tail period, at least one.  A T-block
-    // tail workgroup fills a whole CU (1024 lanes x 128 VGPRs), and unconfined
+    // tail workgroup fills a whole CU (512 lanes x 197 VGPRs), and unconfined
     // it locks the latency-critical head steps out of the chip for its whole
     // duration (measured: a 197 us head step behind a 193 us tail).  With the
     // tail's far-row windows cfg3's tail fits one unit (32 CUs):
