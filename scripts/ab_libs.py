@@ -86,3 +86,6 @@ for path, r, hr in zip(a.libs, res, host):
     print(f"{path}: median {us:.2f} us/step (min {min(r):.2f}) -> {Cn * B / us:.1f} MS/s; "
           f"host enqueue {statistics.median(hr):.2f} us/step")
 print("outputs bit-identical across builds:", same)
+for lib, h, _ in handles:  # (destroyed before exit: launch timelines are written at destroy)
+    lib.fftconv_uniform_destroy.argtypes = [C.c_void_p]
+    lib.fftconv_uniform_destroy(h)

@@ -1,0 +1,76 @@
+"""`process_device_steps` over the generic / pipelined step (a uniform batch
+without lookahead) and over a two-stage's aligned calls equals the same calls
+made one by one, bitwise, and the oracle (src/fft_convolver.rs:215-295,
+:412-495) -- through a non-finite block in one channel, and for the two-stage
+from a start off a period boundary."""
+import numpy as np
+import pytest
+import torch
+
+from common import assert_close, ir, white
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_steps(conv, x, n, K):
+    C = x.shape[0]
+    dev = torch.device("cuda:0")
+    xd = torch.from_numpy(np.ascontiguousarray(x.reshape(C, K, n).transpose(1, 0, 2))).to(dev)  # [K][C][n]
+    yd = torch.empty_like(xd)
+    s = torch.cuda.Stream(dev)
+    conv.process_device_steps(xd.data_ptr(), n, C * n, yd.data_ptr(), n, C * n, n, K, s.cuda_stream)
+    s.synchronize()
+    return yd.cpu().numpy().transpose(1, 0, 2).reshape(C, K * n)
+
+
+@pytest.mark.parametrize("B,L", [(64, 4096), (128, 3000), (512, 6000)])
+def test_uniform_device_steps(amd, oracle_mod, B, L):
+    rng = np.random.default_rng(800 + B)
+    C, K = 5, 90
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    x = np.stack([white(rng, K * B) for _ in range(C)])
+    x[3, 40 * B + 7] = np.nan  # a failed C2R mid-run
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    assert conv.lookahead_parts() == 0
+    y = _device_steps(conv, x, B, K)
+    one = amd.FFTConvolver.init(hs, B, L, channels=C)
+    yh = np.concatenate([one.process(x[:, k * B:(k + 1) * B]) for k in range(K)], axis=1)
+    assert np.array_equal(y, yh, equal_nan=True)
+    for c in (0, 3):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        r = np.concatenate([ref.process(x[c, k * B:(k + 1) * B]) for k in range(K)])
+        assert np.array_equal(np.isnan(y[c]), np.isnan(r))
+        m = ~np.isnan(r)
+        assert_close(y[c][m], r[m], what=f"channel {c}")
+    for c in range(C):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        for k in range(K):
+            ref.process(x[c, k * B:(k + 1) * B])
+        assert conv.channel_state(c) == (ref.current, ref.active_seg_count, ref.fill)
+
+
+@pytest.mark.parametrize("head,L", [(64, 20000), (32, 12000)])
+def test_twostage_device_steps(amd, oracle_mod, head, L):
+    rng = np.random.default_rng(810 + head)
+    C = 3
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.TwoStageFFTConvolver.init(hs, head, L, channels=C)
+    T = conv.tail_block_size
+    K = 3 * T // head + 5
+    x = np.stack([white(rng, K * head) for _ in range(C)])
+    x[1, (T // head + 3) * head + 5] = np.nan
+    # a partial call first: the runs start off a period boundary
+    first = np.stack([white(rng, head) for _ in range(C)])
+    conv.process(first)
+    y = _device_steps(conv, x, head, K)
+    one = amd.TwoStageFFTConvolver.init(hs, head, L, channels=C)
+    one.process(first)
+    yh = np.concatenate([one.process(x[:, k * head:(k + 1) * head]) for k in range(K)], axis=1)
+    assert np.array_equal(y, yh, equal_nan=True)
+    for c in range(C):
+        ref = oracle_mod.TwoStageFFTConvolver.init(hs[c], head, L)
+        ref.process(first[c])
+        r = np.concatenate([ref.process(x[c, k * head:(k + 1) * head]) for k in range(K)])
+        assert np.array_equal(np.isnan(y[c]), np.isnan(r)), c
+        m = ~np.isnan(r)
+        assert_close(y[c][m], r[m], what=f"channel {c}")
