@@ -1581,15 +1581,37 @@ int lg_tables(int dev, int log2m, LgTab *out) {
 // (m^2 mod 2n in integers, the angle in f64) and the spectrum of the chirp
 // filter b (b_m = b_{P-m} = w_m, m < n) by an f64 FFT on the host, both
 // rounded to f32 once; the filter in the device FFT's bin order.  One set per
-// (device, n), kept for the process.
+// (device, n) in a cache of at most kBluesteinCacheBytes of device memory:
+// the least recently used sets are freed when a new length would pass it.
+// The caller holds bluestein_mutex() from this lookup until its kernels are
+// enqueued, so a set being freed was last used by work already on a stream,
+// and the eviction waits for that device before hipFree.  The first use of a
+// length uploads on the caller's stream and waits for that stream only.
 constexpr size_t kMaxBluestein = (size_t)1 << 21;  // P = 2^22 at most
-int bluestein_tables(int dev, size_t n, int log2p, const float2 **chirp, const float2 **filt) {
+constexpr size_t kBluesteinCacheBytes = (size_t)256 << 20;
+std::mutex &bluestein_mutex() {
     static std::mutex mu;
-    static std::map<std::pair<int, size_t>, float2 *> tabs;
-    std::lock_guard<std::mutex> lk(mu);
+    return mu;
+}
+int bluestein_tables(int dev, size_t n, int log2p, hipStream_t s, const float2 **chirp, const float2 **filt) {
+    struct Tab { float2 *p; size_t bytes; unsigned long long used; };
+    static std::map<std::pair<int, size_t>, Tab> tabs;
+    static size_t total = 0;
+    static unsigned long long clock = 0;
     const size_t P = (size_t)1 << log2p;
     auto it = tabs.find({dev, n});
     if (it == tabs.end()) {
+        const size_t bytes = (n + P) * sizeof(float2);
+        while (!tabs.empty() && total + bytes > kBluesteinCacheBytes) {
+            auto lru = tabs.begin();
+            for (auto j = tabs.begin(); j != tabs.end(); ++j)
+                if (j->second.used < lru->second.used) lru = j;
+            DeviceGuard g(lru->first.first);
+            (void)hipDeviceSynchronize();  // kernels enqueued with this set have finished
+            (void)hipFree(lru->second.p);
+            total -= lru->second.bytes;
+            tabs.erase(lru);
+        }
         std::vector<double> wr(n), wi(n);
         for (size_t m = 0; m < n; ++m) {
             const unsigned long long q = ((unsigned long long)m * m) % (2ull * n);
@@ -1638,16 +1660,19 @@ int bluestein_tables(int dev, size_t n, int log2p, const float2 **chirp, const f
             t[n + pos] = make_float2((float)br[k], (float)bi[k]);
         }
         float2 *d = nullptr;
-        HIP_TRY(hipMalloc((void **)&d, t.size() * sizeof(float2)));
-        hipError_t e = hipMemcpy(d, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice);
+        HIP_TRY(hipMalloc((void **)&d, bytes));
+        hipError_t e = hipMemcpyAsync(d, t.data(), bytes, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);  // (t is freed on return)
         if (e != hipSuccess) {
             (void)hipFree(d);
             return fail(FFTCONV_E_DEVICE, std::string("Bluestein tables: ") + hipGetErrorString(e));
         }
-        it = tabs.emplace(std::make_pair(dev, n), d).first;
+        it = tabs.emplace(std::make_pair(dev, n), Tab{d, bytes, 0}).first;
+        total += bytes;
     }
-    *chirp = it->second;
-    *filt = it->second + n;
+    it->second.used = ++clock;
+    *chirp = it->second.p;
+    *filt = it->second.p + n;
     return FFTCONV_OK;
 }
 
@@ -1674,7 +1699,8 @@ int fft_rows(int device, size_t n, size_t rows, const float *din, size_t is, flo
         const size_t P = std::max<size_t>(2, next_pow2(2 * n - 1));
         const int lp = ilog2(P);
         const float2 *chirp = nullptr, *filt = nullptr, *twP = nullptr;
-        if (int r = bluestein_tables(device, n, lp, &chirp, &filt)) return r;
+        std::lock_guard<std::mutex> lk(bluestein_mutex());  // until the kernels are enqueued
+        if (int r = bluestein_tables(device, n, lp, s, &chirp, &filt)) return r;
         LgTab t{};
         float2 *scr = nullptr;
         size_t batch = rows;

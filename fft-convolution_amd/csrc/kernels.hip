@@ -153,21 +153,9 @@ __device__ __attribute__((noinline)) bool c2r_rejects(const float2 *Hc, const fl
 // aux 2 = nontemporal.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-// FFTCONV_DEBUG_BOUNDS (debug builds only): report out-of-range stream rows
-// and window/state indices with printf instead of touching the memory
-#ifdef FFTCONV_DEBUG_BOUNDS
-// one out-of-line report for every check (a printf inlined at each of the
-// hundreds of inlined load sites made the debug build compile for hours)
-__device__ __attribute__((noinline)) void dbg_bounds(int site, int v0, int v1, int v2, int v3) {
-    printf("BOUNDS site %d blk %d tid %d: %d %d %d %d\n", site, (int)blockIdx.x, (int)threadIdx.x, v0, v1, v2, v3);
-}
-#define DBG_CHECK(cond, site, v0, v1, v2, v3)       \
-    do {                                            \
-        if (!(cond)) dbg_bounds(site, v0, v1, v2, v3); \
-    } while (0)
-#else
-#define DBG_CHECK(cond, site, v0, v1, v2, v3) do {} while (0)
-#endif
+// FFTCONV_DEBUG_BOUNDS (debug builds only): DBG_CHECK (kernels.hpp) reports
+// out-of-range stream rows and window/state indices with printf instead of
+// touching the memory
 struct RowStream {
     __amdgpu_buffer_rsrc_t r;
 #ifdef FFTCONV_DEBUG_BOUNDS

@@ -3,6 +3,24 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+// FFTCONV_DEBUG_BOUNDS (debug builds only, Makefile target debug-bounds):
+// DBG_CHECK(cond, site, v0..v3) reports a failed index check with printf.
+// One out-of-line report per translation unit (a printf inlined at each of
+// the hundreds of inlined load sites made the debug build compile for hours).
+#ifdef FFTCONV_DEBUG_BOUNDS
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+static __device__ __attribute__((noinline)) void dbg_bounds(int site, int v0, int v1, int v2, int v3) {
+    printf("BOUNDS site %d blk %d tid %d: %d %d %d %d\n", site, (int)blockIdx.x, (int)threadIdx.x, v0, v1, v2, v3);
+}
+#endif
+#define DBG_CHECK(cond, site, v0, v1, v2, v3)          \
+    do {                                               \
+        if (!(cond)) dbg_bounds(site, v0, v1, v2, v3); \
+    } while (0)
+#else
+#define DBG_CHECK(cond, site, v0, v1, v2, v3) do {} while (0)
+#endif
+
 namespace fftconv {
 
 enum : int {

@@ -214,6 +214,8 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
         const ProcJob &J = p.J;
         const Chunk ch = lg_chunk<LM>(J, row);
         if (!ch.go) return;
+        DBG_CHECK(ch.cur >= 0 && ch.cur < J.S && ch.act <= J.S && ch.k > 0 && ch.fill + ch.k <= M, 50, ch.cur, ch.act,
+                  ch.fill, ch.k);  // (site 50: pass A's chunk and FDL row)
         Y = J.X + (row * (size_t)J.S + (size_t)ch.cur) * M;
         // copy_and_pad of the input buffer (:229-234): sample i is the chunk's
         // input inside [fill, fill + k), else the buffered sample (or 0)
@@ -231,6 +233,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
         }
     } else if constexpr (MODE == LG_IR) {
         const size_t ch = row / p.nseg, s = row % p.nseg;
+        DBG_CHECK(p.nseg <= p.S, 51, (int)s, p.nseg, p.S, p.chan0);  // (site 51: an IR segment row)
         Y = p.H + ((p.chan0 + ch) * (size_t)p.S + s) * M;
         const float *src = p.src + ch * p.src_stride;
         const long long base = (long long)s * M;  // (B = M samples per segment)
@@ -254,6 +257,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
     for (int e = tid; e < LG_E; e += LG_NT) {
         const int t = e & (TC - 1), k1 = e / TC;
         const int n2 = c0 + t;
+        DBG_CHECK(k1 < M1 && n2 < M2, 52, k1, n2, tile, (int)row);  // (site 52: pass A's Y position)
         Y[(size_t)k1 * M2 + n2] = cmul(R[e], p.tb.twM[(n2 * k1) & (M - 1)]);
     }
 }
@@ -318,6 +322,7 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
     if constexpr (MODE == LG_CONV) {
         ch = lg_chunk<LM>(p.J, row);
         if (!ch.go) return;
+        DBG_CHECK(ch.cur >= 0 && ch.cur < p.J.S && ch.act <= p.J.S, 53, ch.cur, ch.act, p.J.S, (int)row);  // (site 53)
         Yr = p.J.X + (row * (size_t)p.J.S + (size_t)ch.cur) * M;
     } else if constexpr (MODE == LG_IR) {
         const size_t c = row / p.nseg, s = row % p.nseg;
@@ -378,16 +383,50 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
             // pre_multiplied = sum_{i=1}^{act-1} H[i] (.) X[(current + i) % act] (:244-255)
 #pragma unroll
             for (int u = 0; u < EP; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            // RU rows in flight per thread (RU x EP x 2 float4 loads issued
+            // before their MACs), then the MACs in row order: the same sums
+            // in the same order as one row at a time
+#ifdef FFTCONV_LG_RU
+            constexpr int RU = FFTCONV_LG_RU;  // (A/B builds)
+#else
+            constexpr int RU = EP >= 8 ? 1 : 8 / EP;
+#endif
+            size_t q[EP];
+#pragma unroll
+            for (int u = 0; u < EP; ++u) q[u] = rp.pos(2 * tid + 2 * LG_NT * u) / 2;
+            const float4 *H4 = reinterpret_cast<const float4 *>(Hc);
+            const float4 *X4 = reinterpret_cast<const float4 *>(Xc);
+            constexpr size_t RF = (size_t)M / 2;  // float4 per row
             int xi = (ch.cur + 1) % ch.act;  // (current may exceed act after an update shrank it)
-            for (int i = 1; i < ch.act; ++i) {
-                const float4 *hr = reinterpret_cast<const float4 *>(Hc + (size_t)i * M);
-                const float4 *xr = reinterpret_cast<const float4 *>(Xc + (size_t)xi * M);
+            int i = 1;
+            for (; i + RU <= ch.act; i += RU) {
+                float4 hv[RU][EP], xv[RU][EP];
+                int xr = xi;
+#pragma unroll
+                for (int r = 0; r < RU; ++r) {
+#pragma unroll
+                    for (int u = 0; u < EP; ++u) {
+                        DBG_CHECK(xr >= 0 && xr < ch.act && 2 * q[u] + 1 < (size_t)M, 54, xr, ch.act, (int)q[u],
+                                  i + r);  // (site 54: a MAC row)
+                        hv[r][u] = ntload(H4 + (size_t)(i + r) * RF + q[u]);
+                        xv[r][u] = ntload(X4 + (size_t)xr * RF + q[u]);
+                    }
+                    if (++xr == ch.act) xr = 0;
+                }
+#pragma unroll
+                for (int r = 0; r < RU; ++r)
+#pragma unroll
+                    for (int u = 0; u < EP; ++u)
+                        acc[u] = mac4(acc[u], hv[r][u], xv[r][u], tid == 0 && u == 0 && rp.w == 0);
+                xi = xr;
+            }
+            for (; i < ch.act; ++i) {
                 float4 hv[EP], xv[EP];
 #pragma unroll
                 for (int u = 0; u < EP; ++u) {
-                    const size_t q = rp.pos(2 * tid + 2 * LG_NT * u) / 2;
-                    hv[u] = ntload(hr + q);
-                    xv[u] = ntload(xr + q);
+                    DBG_CHECK(xi >= 0 && xi < ch.act, 54, xi, ch.act, (int)q[u], i);
+                    hv[u] = ntload(H4 + (size_t)i * RF + q[u]);
+                    xv[u] = ntload(X4 + (size_t)xi * RF + q[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < EP; ++u) acc[u] = mac4(acc[u], hv[u], xv[u], tid == 0 && u == 0 && rp.w == 0);
@@ -522,6 +561,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
                     if (j >= lo && j < hi) ibc[j] = inc[ch.processed + j - lo];
                     continue;
                 }
+                DBG_CHECK(j < B && (j < lo || j >= hi || ch.processed + j - lo < J.n), 56, j, lo, hi, ch.processed);
                 if (j >= lo && j < hi) outc[ch.processed + j - lo] = (q ? R[e].y : R[e].x) * invN + ovc[j];  // :270-274
                 if (complete) {
                     if (ch.flags & FLAG_INBUF) ibc[j] = 0.f;  // :280
@@ -544,6 +584,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
         if (tid == 0) {
             __threadfence();
             const int old = __hip_atomic_fetch_add(pg + 3, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            DBG_CHECK(old >= 0 && old < G::NTILE, 55, old, G::NTILE, (int)row, 0);  // (site 55: the arrival counter)
             if (old == G::NTILE - 1) {
                 pg[3] = 0;
                 int cur = ch.cur, fill = ch.fill, flags = ch.flags & ~(LA_MASK | SEQ_MASK | FLAG_PRE);
@@ -735,6 +776,7 @@ __device__ __forceinline__ float2 bs_src(const BsPass &p, const float *in, int j
     if (!p.inverse) return make_float2(in[j], 0.f);
     const int nb = p.n / 2;  // last bin
     // conj(X_full[j]): X_full[j] = bin j (j <= n/2) or conj(bin n - j)
+    DBG_CHECK(j >= 0 && j < p.n, 57, j, p.n, 0, 0);  // (site 57: a Bluestein source index)
     if (j <= nb) {
         const bool real = j == 0 || (2 * j == p.n);  // DC / Nyquist: imaginary part taken as 0
         return make_float2(in[2 * j], real ? 0.f : -in[2 * j + 1]);
@@ -746,6 +788,7 @@ __device__ __forceinline__ bool bs_flagged(const BsPass &p, const float *in) {
 }
 // X_m = conj(w_m) c_m / P written out (forward: bins m <= n/2; inverse: sample m)
 __device__ __forceinline__ void bs_out(const BsPass &p, float *o, int m, float2 c, float invP, bool flagged) {
+    DBG_CHECK(m >= 0 && m < p.n, 58, m, p.n, 0, 0);  // (site 58: a Bluestein output index)
     const float2 x = cmulc(make_float2(c.x * invP, c.y * invP), p.w[m]);
     if (!p.inverse) {
         if (2 * m > p.n) return;
@@ -817,7 +860,10 @@ __global__ __launch_bounds__(LG_NT) void bs_rows(BsPass p) {
     __syncthreads();
     float2 *F = bfft<G::L2, 1, false, false>(b0, b1, p.tb.twB, tid);
     float2 *Gb = F == b0 ? b1 : b0;
-    for (int e = tid; e < M2; e += LG_NT) Gb[e] = cmul(F[e], p.bf[(size_t)k1 * M2 + e]);
+    for (int e = tid; e < M2; e += LG_NT) {
+        DBG_CHECK((size_t)k1 * M2 + e < (size_t)P, 59, k1, e, M2, P);  // (site 59: the filter spectrum)
+        Gb[e] = cmul(F[e], p.bf[(size_t)k1 * M2 + e]);
+    }
     __syncthreads();
     const float2 *R = bfft<G::L2, 1, false, true>(Gb, F, p.tb.twB, tid);
     for (int e = tid; e < M2; e += LG_NT) Y[e] = cmulc(R[e], p.tb.twM[(e * k1) & (P - 1)]);

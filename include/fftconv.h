@@ -61,22 +61,32 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
 
 /* ---- Fft (src/fft_convolver.rs:7-50) ----------------------------------- */
 /* The reference's public real FFT (realfft's RealToComplex / ComplexToReal of
- * length n) as batched device transforms -- the convolver's own kernels, so a
- * spectrum here is bit-identical to the convolver's.  n: power of two in
- * 2..2^23 (n > 16384: the four-step passes of the long-block path).
+ * length n; Fft::init takes any usize, :30-34) as batched device transforms.
+ * n: any length in 1..2^21, or a power of two up to 2^23.
+ *   - A power of two runs the convolver's own kernels (n > 16384: the
+ *     four-step passes of the long-block path), so a spectrum here is
+ *     bit-identical to the convolver's.
+ *   - Any other length runs Bluestein's chirp-z transform over power-of-two
+ *     FFTs of P >= 2n-1 points (its tables are cached per length, at most
+ *     256 MiB of device memory, least recently used first out).  Those
+ *     spectra are within f32 rounding of an f64 DFT, not bit-identical to any
+ *     convolver kernel (the convolver's block sizes are powers of two).
+ * A row of bins is 2*(n/2+1) floats: n+2 for even n, n+1 for odd n.
  * Forward (Fft::forward :36-39): rows of n reals -> n/2+1 bins,
- * interleaved (re, im), unnormalised, DC / Nyquist imaginary parts 0.
+ * interleaved (re, im), unnormalised, DC (and, for even n, Nyquist)
+ * imaginary parts 0.
  * Inverse (Fft::inverse :41-49): n/2+1 bins -> n reals divided by n;
  * d_status[row] (optional) = 1 where realfft returns FftError::InputValues
- * (non-zero DC / Nyquist imaginary part; the transform runs with those parts
- * as 0).  Such a row is NOT divided by n: Fft::inverse returns the error
- * through `?` (:42) before its normalisation loop (:44-46).  Strides in
- * floats; enqueued on `hip_stream` (NULL = legacy stream). */
+ * (non-zero DC imaginary part, or for even n a non-zero Nyquist imaginary
+ * part; the transform runs with those parts as 0).  Such a row is NOT divided
+ * by n: Fft::inverse returns the error through `?` (:42) before its
+ * normalisation loop (:44-46).  Strides in floats; enqueued on `hip_stream`
+ * (NULL = legacy stream). */
 int fftconv_fft_forward(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
                         size_t out_stride, void *hip_stream);
 int fftconv_fft_inverse(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
                         size_t out_stride, int *d_status, void *hip_stream);
-/* Host-memory forms, rows packed ([rows][n] reals, [rows][n+2] bin floats);
+/* Host-memory forms, rows packed ([rows][n] reals, [rows][2*(n/2+1)] bin floats);
  * synchronous (temporary device buffers: not for the real-time path). */
 int fftconv_fft_forward_host(int device, size_t n, size_t rows, const float *input, float *output);
 int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *input, float *output, int *status);

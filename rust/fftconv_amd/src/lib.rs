@@ -237,9 +237,12 @@ impl GpuFFTConvolverBatch {
 }
 
 /// Fft (src/fft_convolver.rs:7-50): realfft's R2C / C2R of length n on the
-/// GPU -- the convolver's own transforms, so a spectrum here is bit-identical
-/// to the row a handle holds.  n is a power of two in 2..2^23 (the library
-/// returns FFTCONV_E_UNSUPPORTED, and this panics, otherwise).
+/// GPU.  n is any length in 1..2^21, or a power of two up to 2^23 (the library
+/// returns FFTCONV_E_UNSUPPORTED, and this panics, otherwise).  A power of two
+/// runs the convolver's own transforms, so its spectrum is bit-identical to
+/// the row a handle holds; any other length runs Bluestein's chirp-z
+/// transform (within f32 rounding of an f64 DFT, not bit-identical to a
+/// convolver kernel).
 #[derive(Clone, Default, Debug)]
 pub struct GpuFft {
     n: usize,
@@ -269,7 +272,10 @@ impl GpuFft {
                                           &mut bad)
         });
         if bad != 0 {
-            return Err(FftError::InputValues(input[0].im != 0.0, input[self.n / 2].im != 0.0));
+            // realfft's odd-length C2R checks the DC bin only: input[n/2] is
+            // then an ordinary bin, so its flag is false
+            return Err(FftError::InputValues(input[0].im != 0.0,
+                                             self.n % 2 == 0 && input[self.n / 2].im != 0.0));
         }
         Ok(())
     }

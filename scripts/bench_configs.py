@@ -15,6 +15,9 @@ inputs, HIP events on the launch stream).  Prints one JSON line per config.
   cfg2u: cfg2 (1024 channels, block 256, IR 48000) with update_device() of
         every channel every 128 blocks (the post-update launches under
         rocprofv3 show whether an IR swap costs the process path anything).
+  lg:   the long-block path (csrc/large.hip): lgu = FFTConvolver block 16384,
+        IR 1,000,000, 64 channels; lgt = TwoStageFFTConvolver head 512,
+        IR 200,000 (tail block 16384), 256 channels.
 
 Algorithmic bytes per output sample follow SURVEY.md §8(d).  Each line also
 carries `cpu_baseline` (the oracle port, oracle/fftconv_oracle.c, on a bounded
@@ -54,6 +57,31 @@ def tail0_deferred_bytes_per_block(head, T):
     FDL write), its conv (2), its C2R output (2), input and output (1)."""
     n = S0 = T // head
     return (2 * S0 - 1 + 9 * n) * 8 * head / n
+
+
+GW_P = 8  # far-row windows' split row (csrc/kernels.hpp kGwP)
+
+
+def windowed_bytes(B, L, P=GW_P):
+    """The generic step with far-row windows (1024 <= B <= 8192, DESIGN §4f;
+    csrc/kernels.hip gw_anchor_kernel), per channel-block, in rows of 8 B bytes
+    (B packed complex slots, Nyquist in slot 0's imaginary part):
+      step: H[1..P-1] and their P-1 FDL rows, the window row, H[0], the new
+            FDL row (2P + 1 rows) + input, output, overlap read / write (16 B);
+      anchor, every P blocks: FDL rows at ring offsets 1..act-1, H[P..act-1],
+            and P window rows written (2 act - 1 rows)."""
+    S = -(-L // B)
+    row = 8 * B
+    return row * (2 * P + 1) + row * (2 * S - 1) / P + 16 * B
+
+
+def lg_step_bytes(B, L):
+    """One block of the long-block path (csrc/large.hip), per channel: the
+    canonical bytes (uniform_bytes) plus the four-step passes' own row
+    transfers, in rows of 8 B bytes: pass B re-reads pass A's FDL row and
+    rewrites it as the spectrum, writes pre_multiplied and the V scratch, and
+    pass C reads V back (5 rows)."""
+    return uniform_bytes(B, L) + 5 * 8 * B
 
 
 def run(conv, C, n_in, n_out, steps, warmup, ring, stream, update=None, batched=False):
@@ -121,7 +149,7 @@ def cpu_baseline(kind, C, block, L, every=0, target_s=6.0):
 
 PMC_STEPS = {"3": 256, "5": 256, "2u": 256}
 PMC_WARMUP = {"3": 128, "5": 64, "2u": 200}  # (run()'s warmup per config: cfg3 2T/head, cfg5 64, cfg2u 200)
-PMC_REGEX = "upols_|ir_segments|la_rebuild|tail0_|twostage_accum|crossfade_mix|reset_state"
+PMC_REGEX = "upols_|ir_segments|la_rebuild|tail0_|twostage_accum|crossfade_mix|reset_state|lg_"
 
 
 def pmc_config(cfg):
@@ -211,7 +239,9 @@ def main():
         canon_sample = (uniform_bytes(head, T) + uniform_bytes(head, T) + uniform_bytes(T, L - 2 * T) * head / T) / head
         defer = a.variant < 0 or not (a.variant & 256)  # (VARIANT_T0BLOCK, host.cpp TwoStageCore::t0_defer)
         tail0_b = tail0_deferred_bytes_per_block(head, T) if defer else uniform_bytes(head, T)
-        per_sample = (uniform_bytes(head, T) + tail0_b + uniform_bytes(T, L - 2 * T) * head / T) / head
+        gw = (a.variant < 0 or not (a.variant & 1024)) and 1024 <= T <= 8192 and -(-(L - 2 * T) // T) >= 3 * GW_P
+        tail_b = windowed_bytes(T, L - 2 * T) if gw else uniform_bytes(T, L - 2 * T)
+        per_sample = (uniform_bytes(head, T) + tail0_b + tail_b * head / T) / head
         if a.sweep:
             sets = [dict(kv.split("=") for kv in part.split(",") if kv) for part in a.sweep.split(";")]
             times = [[] for _ in sets]
@@ -237,9 +267,10 @@ def main():
                         "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
                         "bytes_per_sample": round(per_sample, 1),
                         "canonical_bytes_per_sample": round(canon_sample, 1),
-                        "path": "head: one fused launch per call; tail0 deferred to the period end (one pass per "
-                                "period); tail: side stream" if tail0_b != uniform_bytes(head, T) else
-                                "head + tail0: one launch per call; tail: side stream",
+                        "path": ("head: one fused launch per call; tail0 deferred to the period end (one pass per "
+                                 "period); tail: side stream" if tail0_b != uniform_bytes(head, T) else
+                                 "head + tail0: one launch per call; tail: side stream")
+                                + ("; tail far-row windows (model: windowed_bytes)" if gw else ""),
                         "cfg": "3", "model_bytes_per_step": int(per_sample * C * head)})
         del conv
         if not a.no_cpu and not a.pmc_inner:
@@ -320,6 +351,49 @@ def main():
                     "note": "update_device() (IR transform + window rebuild) inside the timed region",
                     "cfg": "2u", "model_bytes_per_step": int(lookahead_bytes_per_channel_block(B, L) * C)})
         del conv, fresh
+    if "lg" in a.configs.split(","):
+        # the long-block path (csrc/large.hip, B >= 16384): passes A / B / C
+        # per chunk + lg_call_end.  lgu: FFTConvolver B 16384, IR 1,000,000
+        # (S 62), 64 channels; lgt: TwoStageFFTConvolver head 512, IR 200,000
+        # (T = 16,384 by :520-526, the tail on the long-block path), 256 channels
+        C, B, L = 64, 16384, 1000000
+        conv = F.FFTConvolver.init(shard.synth_irs(range(C), L), B, L, channels=C)
+        S = conv.seg_count
+        steps = max(8, a.steps2 // 16)
+        t, ev = run(conv, C, B, B, steps, S + 2, 4, s, batched=True)
+        samples = C * B * steps
+        per_sample = lg_step_bytes(B, L) / B
+        out.append({"config": "lgu FFTConvolver on the long-block path", "channels": C, "block": B, "ir": L,
+                    "segments": S, "steps": steps, "MSamples_s": round(samples / t / 1e6, 2),
+                    "us_per_step": round(t / steps * 1e6, 3),
+                    "algorithmic_GBs": round(samples * per_sample / t / 1e9, 1),
+                    "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
+                    "bytes_per_sample": round(per_sample, 1),
+                    "canonical_bytes_per_sample": round(uniform_bytes(B, L) / B, 1),
+                    "path": "lg_cols_fwd -> lg_rows (the FDL MAC) -> lg_cols_inv -> lg_call_end per call",
+                    "cfg": "lgu", "model_bytes_per_step": int(per_sample * C * B)})
+        del conv
+        if not a.no_cpu and not a.pmc_inner:
+            out[-1]["cpu_baseline"] = cpu_baseline("uniform", C, B, L, target_s=4.0)
+        C, head, L = 256, 512, 200000
+        conv = F.TwoStageFFTConvolver.init(shard.synth_irs(range(C), L), head, L, channels=C)
+        T = conv.tail_block_size
+        per = T // head
+        steps = per * max(4, a.steps3 // (8 * per))
+        t, ev = run(conv, C, head, head, steps, 2 * per, per, s, batched=True)
+        samples = C * head * steps
+        per_sample = (uniform_bytes(head, T) + tail0_deferred_bytes_per_block(head, T)
+                      + lg_step_bytes(T, L - 2 * T) * head / T) / head
+        out.append({"config": "lgt TwoStageFFTConvolver, tail on the long-block path", "channels": C, "head": head,
+                    "tail": T, "ir": L, "steps": steps, "MSamples_s": round(samples / t / 1e6, 2),
+                    "us_per_step": round(t / steps * 1e6, 3),
+                    "algorithmic_GBs": round(samples * per_sample / t / 1e9, 1),
+                    "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
+                    "bytes_per_sample": round(per_sample, 1),
+                    "cfg": "lgt", "model_bytes_per_step": int(per_sample * C * head)})
+        del conv
+        if not a.no_cpu and not a.pmc_inner:
+            out[-1]["cpu_baseline"] = cpu_baseline("twostage", C, head, L, target_s=4.0)
     if "2m" in a.configs.split(","):
         # cfg2 with calls of m whole blocks (the reference's process over any
         # output length, src/fft_convolver.rs:222-294): one lookahead launch per

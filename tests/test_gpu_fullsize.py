@@ -21,8 +21,13 @@ def _dev_steps(torch, x, n):
 def test_cfg3_twostage_full_size(amd, oracle_mod):
     """cfg3: TwoStageFFTConvolver head 64 / tail 4096 (compute_tail_block_size,
     src/fft_convolver.rs:520-526), IR 262144, 256 channels, 64-sample calls
-    (src/fft_convolver.rs:412-495) past both tail swaps: 2 T/64 + 12 calls.
-    Channels 0, 127, 255 against oracle.TwoStageFFTConvolver."""
+    (src/fft_convolver.rs:412-495) for 12 tail periods (12 T/64 + 16 calls):
+    the T = 4096 tail convolver (:479-486) then runs 11 blocks, so its
+    far-row windows (one anchor class in 8 per tail step, gw_anchor_kernel)
+    are read by every class past entry, at cfg3 geometry with the tail on its
+    CU-masked side stream beside the head and the deferred tail0 flush.
+    Channels 0..7 (all 8 anchor classes), 127 and 255 against
+    oracle.TwoStageFFTConvolver on every call."""
     import torch
 
     C, H, L = 256, 64, 262144
@@ -31,7 +36,7 @@ def test_cfg3_twostage_full_size(amd, oracle_mod):
     conv = amd.TwoStageFFTConvolver.init(hs, H, L, channels=C)
     T = conv.tail_block_size
     assert T == 4096
-    calls = 2 * T // H + 12
+    calls = 12 * T // H + 16
     x = rng.uniform(-1, 1, (C, calls * H)).astype(np.float32)
     xd = _dev_steps(torch, x, H)
     ys = {}
@@ -46,13 +51,15 @@ def test_cfg3_twostage_full_size(amd, oracle_mod):
         ys[scale] = yd
     assert torch.equal(ys[2.0], 2.0 * ys[1.0])
     y = ys[1.0].cpu().numpy()  # [calls][C][H]
-    for c in (0, 127, 255):
+    for c in (*range(8), 127, 255):
         ref = oracle_mod.TwoStageFFTConvolver.init(hs[c], H, L)
         assert ref.tail_block_size == T
         exp = np.concatenate([ref.process(x[c, k * H:(k + 1) * H]) for k in range(calls)])
         got = y[:, c, :].reshape(-1)
         assert float(np.max(np.abs(exp[2 * T:]))) > 0  # the tail convolver's delay-2T output is live
         assert_close(got, exp, what=f"cfg3 channel {c}")
+        for p in range(2, calls * H // T):  # every tail period past entry, on its own
+            assert_close(got[p * T:(p + 1) * T], exp[p * T:(p + 1) * T], what=f"cfg3 channel {c} period {p}")
 
 
 def test_cfg5_crossfade_full_size(amd, oracle_mod):
