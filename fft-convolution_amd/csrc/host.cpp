@@ -629,6 +629,31 @@ struct UniformCore {
         return FFTCONV_OK;
     }
 
+    // `steps` consecutive process() calls (fftconv_uniform_process_device_steps).
+    // A batch on the generic / pipelined step (no lookahead, no far-row
+    // windows, B <= 512) whose workgroups fit the chip twice over runs them
+    // as ONE launch (upols_run_kernel: each channel loops over its calls,
+    // process_job per call -- the same bits as one launch per call).
+    int process_device_steps(const float *din, size_t is, size_t in_step, float *dout, size_t os, size_t out_step,
+                             size_t n, size_t steps, hipStream_t s) {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
+        if (steps >= 2 && n > 0 && n <= (size_t)INT32_MAX && !la_W && !large && !gw_p && !trace_slots &&
+            C <= 2 * (size_t)ncu && steps <= (size_t)INT32_MAX && run_supported(log2b) &&
+            in_step <= (size_t)LLONG_MAX && out_step <= (size_t)LLONG_MAX) {
+            ProcArgs a{};
+            a.job[0] = job(din, is, dout, os, n);
+            a.tw = tw.p;
+            a.njobs = 1;
+            RunSteps r{(long long)in_step, (long long)out_step, (int)steps};
+            HIP_TRY(launch_process_run(log2b, a, r, (int)C, s));
+            return FFTCONV_OK;
+        }
+        for (size_t k = 0; k < steps; ++k)
+            if (int r = process_device(din + k * in_step, is, dout + k * out_step, os, n, s)) return r;
+        return FFTCONV_OK;
+    }
+
     int process_host(const float *in, size_t in_len, float *out, size_t out_len) {
         if (in_len < out_len) return fail(FFTCONV_E_INVALID, "input slice shorter than output (range end index out of range)");
         if (out_len == 0 || C == 0) return FFTCONV_OK;
@@ -736,6 +761,14 @@ struct TwoStageCore {
     // read one whole tail period later (after the next swap), which is the
     // reference's "might be done in some background thread" (:478).
     hipStream_t side = nullptr;
+    // an unmasked side stream for the tail of a period whose calls ran as
+    // multi-call launches (process_device_steps, upols_run_kernel): those
+    // head workgroups stay resident for the whole run, so the tail may use
+    // every CU beside them (cfg3: 5.34 us per step unmasked vs 9.26 on one
+    // unit, while one launch per call is fastest on one unit: 7.18 vs 8.07;
+    // profiles/r5/r5f_*).  null when `side` is unmasked already.
+    hipStream_t side_open = nullptr;
+    bool period_runs = false;  // this period's calls went through multi-call launches
     hipEvent_t ev_main = nullptr, ev_tail = nullptr;
     bool tail_in_flight = false;
     // tail0 deferred to the end of its period (launch_tail0_flush): the
@@ -755,6 +788,7 @@ struct TwoStageCore {
     ~TwoStageCore() {
         DeviceGuard g(device);
         if (side) { (void)hipStreamSynchronize(side); (void)hipStreamDestroy(side); }
+        if (side_open) { (void)hipStreamSynchronize(side_open); (void)hipStreamDestroy(side_open); }
         if (stream) (void)order.drain(stream);
         head.reset(); tail0.reset(); tail.reset();  // (they borrow `stream`)
         if (stream) (void)hipStreamDestroy(stream);
@@ -790,7 +824,13 @@ struct TwoStageCore {
         int ncu = 0;
         HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         int cus = 0;  // 0 = unmasked
-        if (tail && ncu >= 8) {
+        // A long-block tail (T > 2^kMaxLog2Fused, large.hip) is unmasked: its
+        // passes are many short 256-lane workgroups that leave room for the
+        // head steps, and confined by its byte share its row pass ran at a
+        // fraction of the chip's bandwidth (head 512 / IR 200,000: 59.6 us per
+        // step on one unit of 32 CUs, 28.7 on 3 units, 21.4 unmasked;
+        // profiles/r5/r5d_lgt_tail_units.log)
+        if (tail && ncu >= 8 && !tail->large) {
             // bytes per tail period in B-bin rows: the tail's step (with windows:
             // P-1 near rows of H and X, one window row, and 1/P of an anchor's
             // S H rows, S X rows and P window rows) against T/h head steps
@@ -803,11 +843,19 @@ struct TwoStageCore {
             cus = nx * (ncu / 8);
         }
         // (tuning, read once per handle at creation: FFTCONV_TAIL_CU_DIV=k
-        // confines the tail to ncu/k CUs instead, 1 = unmasked)
+        // confines the tail to ncu/k CUs instead, 1 = unmasked;
+        // FFTCONV_TAIL_CU_UNITS=n to n units of ncu/8, 8 = unmasked)
         if (const char *e = getenv("FFTCONV_TAIL_CU_DIV")) {
             const int k = std::max(1, atoi(e));
             cus = k <= 1 ? 0 : std::max(1, ncu / k);
         }
+        const bool knob = getenv("FFTCONV_TAIL_CU_DIV") || getenv("FFTCONV_TAIL_CU_UNITS");
+        if (const char *e = getenv("FFTCONV_TAIL_CU_UNITS")) {
+            const int n = std::min(8, std::max(1, atoi(e)));
+            cus = n >= 8 ? 0 : n * (ncu / 8);
+        }
+        if (cus > 0 && cus < ncu && !knob)  // (a tuning knob governs every period)
+            HIP_TRY(hipStreamCreateWithFlags(&side_open, hipStreamNonBlocking));
         if (cus <= 0 || cus >= ncu) {
             HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
             return FFTCONV_OK;
@@ -931,12 +979,15 @@ struct TwoStageCore {
         // the previous period's tail result, so wait for that kernel here
         if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(s, ev_tail, 0));
         if (tail) {                                                            // :484-485
+            // (the previous tail, on either side stream, finished before ev_main)
+            hipStream_t ts = period_runs && side_open ? side_open : side;
             HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
-            HIP_TRY(hipStreamWaitEvent(side, ev_main, 0));
-            if (int r = tail->process_device(tail_input(), T, tail_output, T, T, side)) return r;
-            HIP_TRY(hipEventRecord(ev_tail, side));
+            HIP_TRY(hipStreamWaitEvent(ts, ev_main, 0));
+            if (int r = tail->process_device(tail_input(), T, tail_output, T, T, ts)) return r;
+            HIP_TRY(hipEventRecord(ev_tail, ts));
             tail_in_flight = true;
         }
+        period_runs = false;
         tin_idx ^= 1;  // the next period fills the other buffer while the tail reads this one
         tail_input_fill = 0;                                                   // :488-491
         precalculated_pos = 0;
@@ -1005,6 +1056,47 @@ struct TwoStageCore {
                 if (int r = end_of_period(s)) return r;
             }
             processed += processing;
+        }
+        return FFTCONV_OK;
+    }
+
+    // `steps` consecutive process() calls (fftconv_twostage_process_device_steps).
+    // Aligned head-block calls inside one tail period, with tail0 deferred,
+    // run as ONE launch (upols_run_kernel: each channel loops over the calls,
+    // process_job per call -- the same bits as one launch per call); the
+    // period's end and every other call shape go through process_device.
+    int process_device_steps(const float *din, size_t is, size_t in_step, float *dout, size_t os, size_t out_step,
+                             size_t len, size_t steps, hipStream_t s) {
+        size_t k = 0;
+        while (k < steps) {
+            const bool aligned = len == head_bs && tail_input_fill % head_bs == 0 && tail_input_fill + len <= T &&
+                                 head->log2b <= kMaxLog2Fused;
+            const size_t left = aligned ? (T - tail_input_fill) / head_bs : 0;
+            // (the period's last call goes through process_device, which ends it)
+            const size_t nrun = std::min(steps - k, left > 0 ? left - 1 : 0);
+            if (aligned && nrun >= 2 && t0_defer && tail0 && run_supported(head->log2b) && !head->trace_slots &&
+                nrun <= (size_t)INT32_MAX && in_step <= (size_t)LLONG_MAX && out_step <= (size_t)LLONG_MAX) {
+                ProcArgs a{};
+                a.job[0] = head->job(din + k * in_step, is, dout + k * out_step, os, len);  // :417
+                a.job[0].add0 = tail_precalculated0 + precalculated_pos;                // :439-445
+                a.job[0].add1 = tail_precalculated + precalculated_pos;                 // :448-454
+                a.job[0].add_stride = (long long)T;
+                a.job[0].tin = tail_input() + tail_input_fill;                         // :459-461
+                a.job[0].tin_stride = (long long)T;
+                a.njobs = 1;
+                a.tw = head->tw.p;
+                RunSteps r{(long long)in_step, (long long)out_step, (int)nrun};
+                HIP_TRY(launch_process_run(head->log2b, a, r, (int)C, s));
+                period_runs = true;
+                if (t0_n == 0) t0_off = tail_input_fill;  // :464-472, deferred
+                t0_n += nrun;
+                precalculated_pos += nrun * len;
+                tail_input_fill += nrun * len;
+                k += nrun;
+                continue;
+            }
+            if (int r = process_device(din + k * in_step, is, dout + k * out_step, os, len, s)) return r;
+            ++k;
         }
         return FFTCONV_OK;
     }
@@ -1827,7 +1919,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len) {
 }
 
 int fftconv_set_kernel_variant(int variant) {
-    if (variant > 2047 || variant < -1) return fail(FFTCONV_E_INVALID, "variant must be 0..2047 (or -1 = auto)");
+    if (variant > 4095 || variant < -1) return fail(FFTCONV_E_INVALID, "variant must be 0..4095 (or -1 = auto)");
     set_variant(variant);
     return FFTCONV_OK;
 }
@@ -1913,11 +2005,7 @@ int fftconv_uniform_process_device_steps(fftconv_uniform *h, const float *d_inpu
     DeviceGuard g(h->core.device);
     hipStream_t s = pick(hip_stream, h->core.stream);
     if (int r = h->core.order.enter(s)) return r;
-    for (size_t k = 0; k < steps; ++k) {
-        if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
-            return r;
-    }
-    return FFTCONV_OK;
+    return h->core.process_device_steps(d_input, in_stride, in_step, d_output, out_stride, out_step, len, steps, s);
 }
 fftconv_uniform *fftconv_uniform_clone(const fftconv_uniform *h) {
     if (!h) { set_error("null handle"); return nullptr; }
@@ -1988,11 +2076,7 @@ int fftconv_twostage_process_device_steps(fftconv_twostage *h, const float *d_in
     DeviceGuard g(h->core.device);
     hipStream_t s = pick(hip_stream, h->core.stream);
     if (int r = h->core.order.enter(s)) return r;
-    for (size_t k = 0; k < steps; ++k) {
-        if (int r = h->core.process_device(d_input + k * in_step, in_stride, d_output + k * out_step, out_stride, len, s))
-            return r;
-    }
-    return FFTCONV_OK;
+    return h->core.process_device_steps(d_input, in_stride, in_step, d_output, out_stride, out_step, len, steps, s);
 }
 fftconv_twostage *fftconv_twostage_clone(const fftconv_twostage *h) {
     if (!h) { set_error("null handle"); return nullptr; }

@@ -1025,6 +1025,35 @@ __global__ __launch_bounds__(NT, NT == 512 ? 2 : 4) void upols_process_kernel(Pr
 }
 
 // ---------------------------------------------------------------------------
+// A run of consecutive process() calls in ONE launch (process_device_steps of
+// a TwoStageFFTConvolver inside one tail period): call k is job[0] with its
+// input / output advanced by k steps and its two-stage slices (tail
+// precalculated, tail_input) by k blocks.  Channels are independent, so each
+// workgroup loops over its channel's calls with no grid-wide sync: call k+1
+// reads the state, FDL row, pre_multiplied and overlap call k stored, which
+// the barrier between calls makes visible to every wave of the workgroup.
+// The body is process_job, the one-call kernel's, so the bits are the same.
+// The kernel boundary between calls goes away (cfg3's head: ~1 us of its
+// ~4.9 us per launch).  At most 2 workgroups per CU (256 VGPRs):
+// the loop keeps its addresses live, and a 128-VGPR body spilled (r4p).
+// ---------------------------------------------------------------------------
+template <int LOG2B, int NT, bool NTL>
+__global__ __launch_bounds__(NT, 2) void upols_run_kernel(ProcArgs a, RunSteps r) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const size_t c = blockIdx.x;
+    ProcJob J = a.job[0];
+    for (int k = 0; k < r.n; ++k) {
+        process_job<LOG2B, NT, false, NTL>(a, J, c, J.state[c], smem);
+        __syncthreads();
+        J.in += r.in_step;
+        J.out += r.out_step;
+        if (J.add0) J.add0 += J.n;
+        if (J.add1) J.add1 += J.n;
+        if (J.tin) J.tin += J.n;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Crossfade mix (src/crossfade_convolver.rs:75-77 + Crossfader::mix :242-278
 // + RaisedCosineMixer :160-169), all channels in lockstep.  mix_value is
 // walked by the same sequential f32 additions the reference performs (once
@@ -2110,6 +2139,44 @@ static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t 
 }
 
 template <int LOG2B>
+static hipError_t launch_run_t(const ProcArgs &a, const RunSteps &r, int channels, hipStream_t s) {
+    if constexpr (LOG2B >= 6 && LOG2B <= 9) {
+        constexpr int PNT = proc_nt(LOG2B);
+        using Gm = Geo<LOG2B, PNT>;
+        if (a.njobs != 1 || r.n < 1) return hipErrorInvalidValue;
+        const int var = pick_variant(a, channels, LOG2B);
+        if (var & 1) return hipErrorInvalidValue;  // (zig-zag order: per-call launches only)
+        ProcArgs args = a;
+        args.pipe = (var & VARIANT_NOPIPE) ? 0 : 1;
+        args.lag = pipeline_lag(LOG2B);
+        auto kern = (var & VARIANT_NT) ? upols_run_kernel<LOG2B, PNT, true> : upols_run_kernel<LOG2B, PNT, false>;
+        if (Gm::lds_bytes > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)Gm::lds_bytes);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(kern, dim3(channels), dim3(PNT), Gm::lds_bytes, s, args, r);
+        return hipGetLastError();
+    } else {
+        return hipErrorNotSupported;
+    }
+}
+bool run_supported(int log2b) {
+    if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NORUN)) return false;
+    return log2b >= 6 && log2b <= 9 && !(scan_variant_set() && (g_variant & VARIANT_ZIGZAG));
+}
+hipError_t launch_process_run(int log2b, const ProcArgs &a, const RunSteps &r, int channels, hipStream_t s) {
+    if (channels <= 0) return hipSuccess;
+    switch (log2b) {
+        case 6: return launch_run_t<6>(a, r, channels, s);
+        case 7: return launch_run_t<7>(a, r, channels, s);
+        case 8: return launch_run_t<8>(a, r, channels, s);
+        case 9: return launch_run_t<9>(a, r, channels, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
+template <int LOG2B>
 static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s) {
     if constexpr (LOG2B >= 6 && LOG2B <= 9) {
         constexpr int B = 1 << LOG2B, KT = 256 / (B / 2), NT = proc_nt(LOG2B);
@@ -2475,7 +2542,7 @@ hipError_t launch_state_flags(int4 *state, int channels, int set, int clear, hip
     return hipGetLastError();
 }
 
-void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 2047); }
+void set_variant(int v) { g_variant = v < 0 ? VARIANT_AUTO : (v & 4095); }
 bool gw_windows_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_NOGW); }
 bool tail0_defer_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_T0BLOCK); }
 bool la_fuse_mix_allowed() { return g_variant == VARIANT_AUTO || !(g_variant & VARIANT_NOFMIX); }

@@ -66,6 +66,7 @@ enum : int {
     VARIANT_T0BLOCK = 256,  // two-stage: tail0 per block (else deferred to the end of its period), read at create
     VARIANT_T0FUSED = 512,  // deferred tail0 at B = 64: one fused flush kernel instead of five (bit-identical)
     VARIANT_NOGW = 1024,    // B >= 1024: no far-row windows, every step sums its far rows itself (tests)
+    VARIANT_NORUN = 2048,   // process_device_steps: one launch per call (else a run of a period's calls per launch)
     VARIANT_AUTO = 0x7fffffff
 };
 void set_variant(int v);
@@ -227,6 +228,15 @@ struct FftArgs {
 hipError_t launch_fft_rows(int log2m, bool inverse, const FftArgs &a, int rows, hipStream_t s);
 
 hipError_t launch_process(int log2b, const ProcArgs &a, int channels, hipStream_t s);
+// a run of r.n consecutive one-job process() calls in one launch
+// (upols_run_kernel, 64 <= B <= 512): call k = job[0] with in / out advanced
+// by k * in_step / out_step floats and add0 / add1 / tin by k * n
+struct RunSteps {
+    long long in_step, out_step;
+    int n;
+};
+bool run_supported(int log2b);
+hipError_t launch_process_run(int log2b, const ProcArgs &a, const RunSteps &r, int channels, hipStream_t s);
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s);
 hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipStream_t s);
 hipError_t launch_crossfade_mix(const CrossfadeMixArgs &a, int channels, hipStream_t s);

@@ -621,7 +621,9 @@ __global__ __launch_bounds__(256) void lg_call_end(ProcJob J) {
     const float *p0 = J.add0 ? J.add0 + c * J.add_stride : nullptr;
     const float *p1 = J.add1 ? J.add1 + c * J.add_stride : nullptr;
     float *ti = J.tin ? J.tin + c * J.tin_stride : nullptr;
-    for (int j = threadIdx.x; j < J.n; j += 256) {
+    // (a standalone call that produced its output: nothing to rewrite)
+    const int nloop = (zero || p0 || ti) ? J.n : 0;
+    for (int j = threadIdx.x; j < nloop; j += 256) {
         float v = zero ? 0.f : outc[j];
         if (p0) {
             v += p0[j];

@@ -114,7 +114,12 @@ int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *inp
  * of each tail period; read when a TwoStageFFTConvolver is created), bit 9 =
  * that end-of-period flush in one fused kernel instead of five (head block
  * 64; bit-identical), bit 10 = no far-row windows for 1024 <= B <= 8192 (every
- * one-block call sums its far rows itself; bit-identical).
+ * one-block call sums its far rows itself; bit-identical), bit 11 =
+ * process_device_steps launches once per call (by default, for 64 <= B <= 512,
+ * a TwoStageFFTConvolver's aligned calls inside one tail period, and the
+ * calls of an FFTConvolver batch on the generic / pipelined step with at most
+ * two channels per CU, run as ONE launch in which each channel's workgroup
+ * loops over its calls; bit-identical).
  * Lookahead (automatic for standalone FFTConvolver batches with
  * 128 <= B <= 512 and >= 40 segments, full-block calls from an empty input
  * buffer): the FDL sum of each block is re-associated in time over a near

@@ -80,7 +80,10 @@ for r in range(a.rounds):
         k = run.k
         torch.cuda.synchronize()
         res[idx].append(e0.elapsed_time(e1) * 1000 / a.steps)
-same = all(torch.equal(handles[0][2], hh[2]) for hh in handles[1:])
+eq = [torch.equal(handles[0][2], hh[2]) for hh in handles[1:]]
+same = all(eq)
+if len(eq) > 1:
+    print("bit-identical to the first handle, per handle:", eq)
 for path, r, hr in zip(a.libs, res, host):
     us = statistics.median(r)
     print(f"{path}: median {us:.2f} us/step (min {min(r):.2f}) -> {Cn * B / us:.1f} MS/s; "

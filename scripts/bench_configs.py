@@ -351,7 +351,8 @@ def main():
                     "note": "update_device() (IR transform + window rebuild) inside the timed region",
                     "cfg": "2u", "model_bytes_per_step": int(lookahead_bytes_per_channel_block(B, L) * C)})
         del conv, fresh
-    if "lg" in a.configs.split(","):
+    cfgs = a.configs.split(",")
+    if "lg" in cfgs or "lgu" in cfgs:
         # the long-block path (csrc/large.hip, B >= 16384): passes A / B / C
         # per chunk + lg_call_end.  lgu: FFTConvolver B 16384, IR 1,000,000
         # (S 62), 64 channels; lgt: TwoStageFFTConvolver head 512, IR 200,000
@@ -375,6 +376,7 @@ def main():
         del conv
         if not a.no_cpu and not a.pmc_inner:
             out[-1]["cpu_baseline"] = cpu_baseline("uniform", C, B, L, target_s=4.0)
+    if "lg" in cfgs or "lgt" in cfgs:
         C, head, L = 256, 512, 200000
         conv = F.TwoStageFFTConvolver.init(shard.synth_irs(range(C), L), head, L, channels=C)
         T = conv.tail_block_size

@@ -62,18 +62,18 @@ def test_no_cpu_fallback_without_device():
 
 def test_kernel_variant_knob_range():
     """fftconv_set_kernel_variant (include/fftconv.h): -1 (automatic) and
-    0..2047 are accepted (bits 0-10), anything else is FFTCONV_E_INVALID; a
+    0..4095 are accepted (bits 0-11), anything else is FFTCONV_E_INVALID; a
     host-only setter, no device needed."""
     import fftconv_amd
 
     try:
-        for v in (0, 64, 128, 255, 511, 1024, 2047):
+        for v in (0, 64, 128, 255, 511, 1024, 2047, 4095):
             fftconv_amd.set_kernel_variant(v)
             assert fftconv_amd.get_kernel_variant() == v
-        for bad in (2048, -2, -255):
+        for bad in (4096, -2, -255):
             with pytest.raises(fftconv_amd.ConvolutionPanic):
                 fftconv_amd.set_kernel_variant(bad)
-            assert fftconv_amd.get_kernel_variant() == 2047
+            assert fftconv_amd.get_kernel_variant() == 4095
     finally:
         fftconv_amd.set_kernel_variant(-1)
     assert fftconv_amd.get_kernel_variant() == -1

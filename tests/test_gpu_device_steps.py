@@ -2,7 +2,10 @@
 without lookahead) and over a two-stage's aligned calls equals the same calls
 made one by one, bitwise, and the oracle (src/fft_convolver.rs:215-295,
 :412-495) -- through a non-finite block in one channel, and for the two-stage
-from a start off a period boundary."""
+from a start off a period boundary.  A two-stage's aligned calls inside a
+tail period run as ONE launch (upols_run_kernel, head 64..512), and so do
+the uniform batch's calls (64 <= B <= 512, no lookahead); every other call
+shape one launch per call."""
 import numpy as np
 import pytest
 import torch
@@ -49,7 +52,7 @@ def test_uniform_device_steps(amd, oracle_mod, B, L):
         assert conv.channel_state(c) == (ref.current, ref.active_seg_count, ref.fill)
 
 
-@pytest.mark.parametrize("head,L", [(64, 20000), (32, 12000)])
+@pytest.mark.parametrize("head,L", [(64, 20000), (32, 12000), (128, 40000), (256, 70000), (512, 200000)])
 def test_twostage_device_steps(amd, oracle_mod, head, L):
     rng = np.random.default_rng(810 + head)
     C = 3

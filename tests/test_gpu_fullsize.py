@@ -50,6 +50,15 @@ def test_cfg3_twostage_full_size(amd, oracle_mod):
         s.synchronize()
         ys[scale] = yd
     assert torch.equal(ys[2.0], 2.0 * ys[1.0])
+    # process_device_steps: the calls inside each tail period as one launch
+    # (upols_run_kernel), bit-identical to one launch per call
+    cv = amd.TwoStageFFTConvolver.init(hs, H, L, channels=C)
+    yr = torch.empty_like(xd)
+    s = torch.cuda.Stream()
+    cv.process_device_steps(xd.data_ptr(), H, C * H, yr.data_ptr(), H, C * H, H, calls, s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(yr, ys[1.0])
+    del cv, yr
     y = ys[1.0].cpu().numpy()  # [calls][C][H]
     for c in (*range(8), 127, 255):
         ref = oracle_mod.TwoStageFFTConvolver.init(hs[c], H, L)
