@@ -275,6 +275,7 @@ struct UniformCore {
     size_t trace_slots = 0, trace_grid = 0;
     std::vector<long long> trace_meta;  // per slot: la_t, grid
     int la_seq = 1;               // launch tag, alternating 1 / 2
+    DevPtr<int> la_probe;         // (tests: FFTCONV_LA_PROBE) post-step state observations
     bool la_all = true;           // next lookahead launch re-anchors every channel
     // long-block path (B > 2^kMaxLog2Fused, large.hip): per-call progress,
     // the inverse's scratch, the geometry's tables; lg_whole: every call
@@ -355,6 +356,10 @@ struct UniformCore {
         if (la_W) {
             const LaDims d = la_dims(log2b, (int)S);
             if (int r = laW.alloc(C * 2 * (size_t)d.pt * B)) return r;
+            if (const char *e = getenv("FFTCONV_LA_PROBE"); e && atoi(e) > 0) {
+                if (int r = la_probe.alloc(1)) return r;
+                HIP_TRY(hipMemset(la_probe.p, 0, sizeof(int)));
+            }
         }
         // launch timelines (tuning only): FFTCONV_LA_TRACE for the lookahead
         // launches of a batch that has them, FFTCONV_PROC_TRACE for the
@@ -554,6 +559,7 @@ struct UniformCore {
         a.la_all = la_all ? 1 : 0;
         a.la_t = (int)(la_t % (unsigned long long)la_dims(log2b, (int)S).per_all);  // (every period divides it)
         a.la_seq = la_seq;
+        a.la_probe_cnt = la_probe.p;
         if (!la_all) return trace_fill(a, s);  // (steady-state launches only: the record is sized for them)
         return FFTCONV_OK;
     }
@@ -2022,6 +2028,14 @@ int fftconv_uniform_synchronize(fftconv_uniform *h) {
 size_t fftconv_uniform_channels(const fftconv_uniform *h) { return h ? h->core.C : 0; }
 int fftconv_uniform_lookahead_parts(const fftconv_uniform *h) { return h ? h->core.la_W : 0; }
 int fftconv_uniform_far_windows(const fftconv_uniform *h) { return h ? h->core.gw_p : 0; }
+int fftconv_uniform_lookahead_probe(const fftconv_uniform *h) {
+    if (!h || !h->core.la_probe.p) return -1;
+    DeviceGuard g(h->core.device);
+    if (h->core.order.drain(h->core.stream) != FFTCONV_OK) return -1;
+    int n = 0;
+    if (hipMemcpy(&n, h->core.la_probe.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return n;
+}
 size_t fftconv_uniform_block_size(const fftconv_uniform *h) { return h ? h->core.B : 0; }
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h) { return h ? h->core.S : 0; }
 int fftconv_uniform_ir_spectrum(const fftconv_uniform *h, size_t channel, size_t segment, float *out) {

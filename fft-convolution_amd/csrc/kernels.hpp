@@ -169,6 +169,10 @@ struct ProcArgs {
     // << 4, HW_ID low 16 bits | XCC_ID << 24, t0, t1} (s_memrealtime, 100 MHz)
     int4 *la_trace;        // this launch's record: [la_trace_grid][4 waves] + phase stamps after it
     int la_trace_grid;
+    // state-word probe (tests only, FFTCONV_LA_PROBE at handle creation): the
+    // anchors wait for the launch's steps and read the state past their L2,
+    // so they observe the post-step word; each such observation is counted
+    int *la_probe_cnt;
     // long-block path (launch_process with log2b > kMaxLog2Fused): the
     // geometry's tables and the chunks to run (an upper bound over channels)
     LgTab lg;

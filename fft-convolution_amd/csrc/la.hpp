@@ -285,24 +285,35 @@ struct LaGeo {
 // the anchor's view of channel c at level lv: its ring position, window and
 // length, or false if this launch opens no window of the level at c.
 //
-// Memory-model assumption (the one shared word of a launch).  The channel's
-// step workgroup stores state[c] once, as ONE 16-byte store from one lane
-// (global_store_dwordx4 of an aligned int4), and an anchor reads it as ONE
-// 16-byte load.  Both are single requests to one 64-byte line: the L2 that
-// holds the line applies the store whole, and a line is written back / filled
-// whole, so a reader on any XCD observes either the pre-step word or the
-// post-step word, never a mix of the two.  (Typically the pre-step one: the
-// writer's L2 keeps the dirty line until the launch's end-of-kernel release,
-// and the reader's L2 was invalidated at launch start.)  Either observation
-// is handled exactly: the launch tag (SEQ_MASK) in the word says which one
-// it is, and both branches below rebuild the same ring position and window.
-// Nothing else of the step is read by an anchor (FDL ages >= 1 only, the
-// other window of each level).
+// The one shared word of a launch.  The channel's step workgroup stores
+// state[c] once, as ONE 16-byte store from one lane (global_store_dwordx4 of
+// an aligned int4), and an anchor reads it as ONE 16-byte load.  Both are
+// single requests to one 64-byte line: the L2 that holds the line applies
+// the store whole, and a line is written back / filled whole, so a reader on
+// any XCD observes either the pre-step word or the post-step word, never a
+// mix.  (The HIP memory model itself does not promise 16-byte single-copy
+// atomicity; this is the CDNA request / line granularity.)  Typically the
+// pre-step word: the writer's L2 keeps the dirty line until the launch's
+// end-of-kernel release, and the reader's L2 was invalidated at launch start.
+// Either observation is handled exactly: the launch tag (SEQ_MASK) in the
+// word says which one it is, and both branches below rebuild the same ring
+// position and window.  The post-step branch is forced and checked bit for
+// bit by tests/test_gpu_lookahead.py::test_lookahead_post_step_state_word
+// (FFTCONV_LA_PROBE: steps fence their store out, anchors wait and read past
+// L2, and the post-step observations are counted).  Nothing else of the step
+// is read by an anchor (FDL ages >= 1 only, the other window of each level).
 template <int LOG2B>
 __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c, int lv, int &cur, int &act, int &win,
                                                 int &d) {
     const ProcJob &J = a.job[jb];
     DBG_CHECK(c >= 0 && c < a.la_channels, 1, c, lv, a.la_channels, 0);  // (site 1: an anchor's channel)
+    if (a.la_probe_cnt && !a.la_rebuild) {
+        // (tests: FFTCONV_LA_PROBE) let the steps of this launch store their
+        // words (each step fences its store out to memory), then read past
+        // this XCD's L2: the post-step branch below is the one taken
+        for (int i = 0; i < 24; ++i) __builtin_amdgcn_s_sleep(127);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
     const int4 st = J.state[c];
     const int sx = __builtin_amdgcn_readfirstlane(st.x), sy = __builtin_amdgcn_readfirstlane(st.y);
     const int sz = __builtin_amdgcn_readfirstlane(st.z), sw = __builtin_amdgcn_readfirstlane(st.w);
@@ -322,6 +333,7 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c
     if (((sw & SEQ_MASK) >> SEQ_SHIFT) == a.la_seq) {
         // this launch's step has already stored the channel's state: it
         // opened the window (this channel is scheduled) iff the level is live
+        if (a.la_probe_cnt && threadIdx.x == 0) atomicAdd(a.la_probe_cnt, 1);
         if (!la_live(sw, lv)) return false;
         cur = sx + 1 == act ? 0 : sx + 1;
         win = (sw & pw) ? 1 : 0;
@@ -877,6 +889,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 else if (la_live(flags, lv)) nf |= la_flag_live(lv);
             }
             JC.state[c] = make_int4(curp, act, 0, nf);
+            if (a.la_probe_cnt) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (tests: the probe)
         }
     } else {
         // output.fill(0); return (:264-267): the block stays in the input

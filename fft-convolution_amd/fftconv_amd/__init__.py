@@ -68,6 +68,7 @@ SIGNATURES = {
     "fftconv_uniform_channels": (_sz, [_vp]),
     "fftconv_uniform_lookahead_parts": (_i, [_vp]),
     "fftconv_uniform_far_windows": (_i, [_vp]),
+    "fftconv_uniform_lookahead_probe": (_i, [_vp]),
     "fftconv_uniform_block_size": (_sz, [_vp]),
     "fftconv_uniform_seg_count": (_sz, [_vp]),
     "fftconv_uniform_ir_spectrum": (_i, [_vp, _sz, _sz, _fp]),
@@ -367,6 +368,11 @@ class FFTConvolver(_Base):
     def far_windows(self) -> int:
         """Window rows per channel of the far-row windows (B >= 1024; 0 = not used)."""
         return int(lib().fftconv_uniform_far_windows(self._h))
+
+    def lookahead_probe(self) -> int:
+        """(tests) post-step state-word observations of the FFTCONV_LA_PROBE
+        launches; -1 when the probe is off."""
+        return int(lib().fftconv_uniform_lookahead_probe(self._h))
 
     def ir_spectrum(self, channel: int, segment: int) -> np.ndarray:
         """segments_ir[segment] of a channel: complex64[B + 1]."""

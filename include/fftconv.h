@@ -207,6 +207,11 @@ int fftconv_uniform_lookahead_parts(const fftconv_uniform *h);
  * anchor every P blocks sums rows >= P for a channel's next P one-block
  * calls; bit-identical to summing them every block), 0 = not used */
 int fftconv_uniform_far_windows(const fftconv_uniform *h);
+/* (tests) with FFTCONV_LA_PROBE=1 in the environment when the handle was
+ * created, the lookahead launches force their anchors to observe the
+ * post-step state word (la.hpp la_anchor_state): the number of such
+ * observations so far; -1 when the probe is off (the default) */
+int fftconv_uniform_lookahead_probe(const fftconv_uniform *h);
 size_t fftconv_uniform_block_size(const fftconv_uniform *h);   /* next_power_of_two(max_block_size) */
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h);
 /* segments_ir[segment] of one channel (src/fft_convolver.rs:92): B+1 bins,

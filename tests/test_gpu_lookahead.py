@@ -359,3 +359,47 @@ def test_lookahead_multi_block_calls(amd, oracle_mod, B):
             assert_close(got[c][m], r[m], what=f"B={B} call {j} (n={n}) ch {c}")
         for c in range(C):
             assert multi.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill), (j, c)
+
+
+@pytest.mark.parametrize("B,C", [(256, 64), (512, 24)])
+def test_lookahead_post_step_state_word(amd, oracle_mod, monkeypatch, B, C):
+    """The anchors' post-step branch (la.hpp la_anchor_state): an anchor that
+    reads its channel's state word after the same launch's step stored it
+    must rebuild the same ring position and window as one that reads the
+    pre-step word.  FFTCONV_LA_PROBE forces it -- every step fences its word
+    out to memory, every anchor waits and then reads past its L2 -- and counts
+    the post-step observations.  The probed batch must be bit-identical to an
+    unprobed one (which sees the pre-step word) through entry, > 2 level-3
+    periods, a partial call and its re-entry, a batch update and a NaN block,
+    and within tolerance of the oracle."""
+    rng = np.random.default_rng(900 + B)
+    L = 67 * B + 5  # S = 68 > 65: all three anchor levels
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    monkeypatch.setenv("FFTCONV_LA_PROBE", "1")
+    probed = amd.FFTConvolver.init(hs, B, L, channels=C)
+    monkeypatch.delenv("FFTCONV_LA_PROBE")
+    plain = amd.FFTConvolver.init(hs, B, L, channels=C)
+    assert probed.lookahead_parts() > 0 and probed.lookahead_probe() == 0
+    assert plain.lookahead_probe() == -1
+    refs = _refs(oracle_mod, hs, B, L)
+    chunks = [B] * 150 + [B // 2, B // 2] + [B] * 20
+    for j, k in enumerate(chunks):
+        if j == 90:
+            hn = np.stack([ir(rng, L) for _ in range(C)])
+            for cv in (probed, plain):
+                cv.update(hn)
+            for c in range(C):
+                refs[c].update(hn[c])
+        x = np.stack([white(rng, k) for _ in range(C)])
+        if j == 120:
+            x[3, 17] = np.nan  # a failed C2R: the channel leaves the lookahead path
+        yp, yq = probed.process(x), plain.process(x)
+        assert np.array_equal(yp, yq, equal_nan=True), f"block {j}: probed != plain"
+        for c in (0, C - 1):
+            assert_close(yp[c], refs[c].process(x[c]), what=f"block {j} ch {c}")
+        for c in range(1, C - 1):
+            refs[c].process(x[c])
+    n = probed.lookahead_probe()
+    # every launch opens C/4 + C/16 + C/64 anchors, so the post-step branch
+    # must have run many times (a same-XCD or written-back step word)
+    assert n >= len(chunks), f"only {n} post-step observations"
