@@ -353,7 +353,8 @@ constexpr bool fft_r2c_q_is_buf1() { return ((fft_nstages<LOG2M>() - 1) & 1) == 
 // S0 > 0: stages [0, S0) already ran (buf0 holds their output; see
 // wave_stage0_padded).  q == nullptr: the spectrum goes to g only.
 // INPLACE: the LDS stages run in buf0 alone (wave_stages_inplace; buf1 unused).
-template <int LOG2M, int S0 = 0, class TW = const float2 *, bool INPLACE = false>
+// GNT: the stores to g are nontemporal (streamed out instead of left dirty in L2).
+template <int LOG2M, int S0 = 0, class TW = const float2 *, bool INPLACE = false, bool GNT = false>
 __device__ __forceinline__ void wave_r2c_post(float2 *buf0, float2 *buf1, TW tw, float2 *q, float2 *g) {
     constexpr int M = 1 << LOG2M;
     constexpr bool R2 = (LOG2M & 1) != 0;     // last stage radix-2 (else radix-4, Ns = M/4)
@@ -398,7 +399,13 @@ __device__ __forceinline__ void wave_r2c_post(float2 *buf0, float2 *buf1, TW tw,
             if (lane == 0) b = i == 0 ? z[0][(NQ - qq) % NQ] : z[(NJ - i) % NJ][NQ - 1 - qq];
             const float2 v = real_post_pair(z[i][qq], b, k, tw);
             if (q) q[k] = v;
-            g[k] = v;
+            if constexpr (GNT) {
+                typedef float f32x2_t __attribute__((ext_vector_type(2)));
+                const f32x2_t w = {v.x, v.y};
+                __builtin_nontemporal_store(w, reinterpret_cast<f32x2_t *>(g + k));
+            } else {
+                g[k] = v;
+            }
         }
     }
 }

@@ -1137,6 +1137,12 @@ __device__ __forceinline__ void mix_walk(const CrossfadeMixArgs &a, float *vtab)
     mix_walk_lane(vtab, a.mix_value0, a.step, a.n);
 }
 
+// IR transform (init / update): H rows stored nontemporal, so the window
+// rebuild behind it finds them written out instead of dirty in L2 (cfg2
+// update: rebuild 277 -> 261 us, cfg2u +1.1 %, profiles/r5/r5i_*)
+#ifndef FFTCONV_IR_NTST
+#define FFTCONV_IR_NTST 1
+#endif
 #include "la.hpp"  // (after the mix helpers: B's lookahead launch can fuse the mix)
 
 __global__ void crossfade_mix_kernel(CrossfadeMixArgs a) {
@@ -1501,7 +1507,8 @@ __global__ __launch_bounds__(64 * ir_nw<LOG2B>()) void ir_segments_wave_kernel(I
         if constexpr (REG) {
             wave_stage0_padded<LOG2B>(cur, curh, bufA);
             wave_sync();
-            wave_r2c_post<LOG2B, 1, TwStaged<LOG2B>, true>(bufA, nullptr, TwStaged<LOG2B>{twl}, nullptr, row);
+            wave_r2c_post<LOG2B, 1, TwStaged<LOG2B>, true, (FFTCONV_IR_NTST != 0)>(bufA, nullptr, TwStaged<LOG2B>{twl},
+                                                                                 nullptr, row);
         } else {
 #pragma unroll
             for (int u = 0; u < NPL; ++u) {

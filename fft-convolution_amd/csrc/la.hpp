@@ -282,6 +282,21 @@ struct LaGeo {
     static constexpr size_t anchor_bytes = (size_t)(LA_NG - 1) * LA_JW * FS * 16;
 };
 
+// store policy of the launch's outputs (FFTCONV_LA_NTST bit 0 = window rows,
+// bit 1 = the step's FDL row, bit 2 = output and overlap samples,
+// nontemporal; the rows are read by later launches, on other XCDs)
+#ifndef FFTCONV_LA_NTST
+#define FFTCONV_LA_NTST 1  // (cfg2 A/B: window rows nontemporal 16.78 -> 16.44 us per step, r5h)
+#endif
+__device__ __forceinline__ void la_wst(float4 *p, float4 v) {
+    if constexpr ((FFTCONV_LA_NTST & 1) != 0) ntst4(p, v);
+    else *p = v;
+}
+__device__ __forceinline__ void la_ost(float *p, float v) {
+    if constexpr ((FFTCONV_LA_NTST & 4) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // the anchor's view of channel c at level lv: its ring position, window and
 // length, or false if this launch opens no window of the level at c.
 //
@@ -399,7 +414,7 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
                 float4 p = acc[j].get();
 #pragma unroll
                 for (int q = 1; q < LA_NG; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * FS + fl]);
-                la_win(a, jb, c, win, LV, P - d + jj, B)[f] = p;
+                la_wst(la_win(a, jb, c, win, LV, P - d + jj, B) + f, p);
             }
         }
     }
@@ -426,7 +441,7 @@ __device__ __forceinline__ void la_level1(const ProcArgs &a, int jb, const float
     la_walk<LOG2B, false, false, JM, la_um(JM)>(acc, hs, xs, f * 16, f == 0, LA_D0 + 1, hi, j0, cur, act);
 #pragma unroll
     for (int j = 0; j < JM; ++j)
-        if (j0 + j >= l * JM && j0 + j < d) la_win(a, jb, c, win, 1, LA_P1 - d + j0 + j, B)[f] = acc[j].get();
+        if (j0 + j >= l * JM && j0 + j < d) la_wst(la_win(a, jb, c, win, 1, LA_P1 - d + j0 + j, B) + f, acc[j].get());
 }
 
 // Level-1 anchor workgroup b (B = 512: the step workgroups have no helper
@@ -717,7 +732,8 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
         // Q (LDS) and FDL row `current` (HBM)
         Q = fft_r2c_q_is_buf1<LOG2B>() ? bufB : bufA;
         Z = fft_r2c_q_is_buf1<LOG2B>() ? bufA : bufB;
-        wave_r2c_post<LOG2B>(bufA, bufB, twl, Q, JC.X + c * rows + (size_t)cur * B);
+        wave_r2c_post<LOG2B, 0, const float2 *, false, (FFTCONV_LA_NTST & 2) != 0>(bufA, bufB, twl, Q,
+                                                                              JC.X + c * rows + (size_t)cur * B);
         la_stamp(a, 1);
     } else {
         if constexpr (TWBAR) __syncthreads();  // (the chain waves' twiddle barrier)
@@ -877,8 +893,8 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 if (JC.add1) v += p1l[j];
             }
             if constexpr (XF == 2) v = mix_select(p0l[j], v, p1l[j]);
-            outc[j] = v;
-            ovc[j] = y[B + j] * invN;  // :283-284
+            la_ost(outc + j, v);
+            la_ost(ovc + j, y[B + j] * invN);  // :283-284
         }
         if (lane == 0) {
             const int curp = cur > 0 ? cur - 1 : act - 1;  // :287-291

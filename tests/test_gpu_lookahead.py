@@ -400,6 +400,7 @@ def test_lookahead_post_step_state_word(amd, oracle_mod, monkeypatch, B, C):
         for c in range(1, C - 1):
             refs[c].process(x[c])
     n = probed.lookahead_probe()
+    print(f"\nB={B} C={C}: {n} post-step state-word observations over {len(chunks)} calls")
     # every launch opens C/4 + C/16 + C/64 anchors, so the post-step branch
     # must have run many times (a same-XCD or written-back step word)
     assert n >= len(chunks), f"only {n} post-step observations"
