@@ -1078,8 +1078,7 @@ struct TwoStageCore {
             const bool aligned = len == head_bs && tail_input_fill % head_bs == 0 && tail_input_fill + len <= T &&
                                  head->log2b <= kMaxLog2Fused;
             const size_t left = aligned ? (T - tail_input_fill) / head_bs : 0;
-            // (the period's last call goes through process_device, which ends it)
-            const size_t nrun = std::min(steps - k, left > 0 ? left - 1 : 0);
+            const size_t nrun = std::min(steps - k, left);
             if (aligned && nrun >= 2 && t0_defer && tail0 && run_supported(head->log2b) && !head->trace_slots &&
                 nrun <= (size_t)INT32_MAX && in_step <= (size_t)LLONG_MAX && out_step <= (size_t)LLONG_MAX) {
                 ProcArgs a{};
@@ -1099,6 +1098,10 @@ struct TwoStageCore {
                 precalculated_pos += nrun * len;
                 tail_input_fill += nrun * len;
                 k += nrun;
+                // a run that ends the period ends it as a per-call aligned call does
+                if (tail_input_fill == T) {
+                    if (int r = end_of_period(s)) return r;
+                }
                 continue;
             }
             if (int r = process_device(din + k * in_step, is, dout + k * out_step, os, len, s)) return r;
