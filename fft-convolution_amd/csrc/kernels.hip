@@ -821,6 +821,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
             flags |= FLAG_PRE;
             break;
         }
+        proc_stamp(a, 0);  // (timelines: pre_multiplied ready)
 
         // forward FFT of the zero-padded input buffer into segments[current]
         // (:229-241): x[i] = chunk sample, else the carried input buffer.
@@ -859,6 +860,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
             Xcur[m] = v;
         }
         __syncthreads();
+        proc_stamp(a, 1);  // (R2C done)
 
         // conv = pre_multiplied + segments[current] (.) segments_ir[0] (:256-261)
         if (owner) {
@@ -885,6 +887,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
         __syncthreads();
         float2 *Y = lds_cfft<LOG2B, NT, true>(Q, Z, tw);
         const float *y = reinterpret_cast<const float *>(Y);
+        proc_stamp(a, 2);  // (C2R done)
 
         // overlap-add (:270-274)
         if (one_block) {
@@ -933,6 +936,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
     // (a live window stays live only across a step that read it and advanced)
     if (tid == 0) J.state[c] = make_int4(cur, act, fill, la_clear(flags, a) | (gwin && !err ? FLAG_GW : 0));
     if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
+    proc_stamp(a, 3);
 }
 
 // ---------------------------------------------------------------------------

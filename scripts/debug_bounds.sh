@@ -1,5 +1,6 @@
 #!/bin/bash
-# The lookahead, two-stage and crossfade GPU tests against the debug build
+# The lookahead, two-stage, crossfade, long-block, device-steps (run kernel)
+# and Bluestein GPU tests against the debug build
 # (make -C fft-convolution_amd debug-bounds): device bounds checks compiled in
 # (FFTCONV_DEBUG_BOUNDS -- an out-of-range stream row, window row or state
 # index prints "BOUNDS site ..." instead of touching memory) and UBSan on the
@@ -11,7 +12,8 @@ export FFTCONV_AMD_LIB="$ROOT/fft-convolution_amd/libfftconv_amd_dbg.so"
 export UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"
 out=gpurun_out/debug_bounds.log
 timeout -k 10 900 python -u -m pytest tests/test_gpu_lookahead.py tests/test_gpu_twostage_defer.py \
-    tests/test_gpu_crossfade_twostage.py tests/test_gpu_large.py tests/test_gpu_fullsize.py tests/test_gpu_windows.py -v \
+    tests/test_gpu_crossfade_twostage.py tests/test_gpu_large.py tests/test_gpu_fullsize.py tests/test_gpu_windows.py \
+    tests/test_gpu_device_steps.py tests/test_gpu_fft_any.py -v \
     --timeout 600 --timeout-method thread -s > "$out" 2>&1
 rc=$?
 echo "pytest rc=$rc"
