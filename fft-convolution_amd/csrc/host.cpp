@@ -582,8 +582,12 @@ struct UniformCore {
 
     // la_mix / mix / mix_tab: crossfade fusion on the lookahead step (ProcArgs::la_mix);
     // the caller only passes them when this call takes the lookahead launch
+    // after_step (optional): recorded once the call's outputs are final, before
+    // the far-row window anchor that follows a one-block step (the two-stage
+    // head reads the tail's output, not its windows)
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t n, hipStream_t s,
-                       int la_mix = 0, const CrossfadeMixArgs *mix = nullptr, float *mix_tab = nullptr) {
+                       int la_mix = 0, const CrossfadeMixArgs *mix = nullptr, float *mix_tab = nullptr,
+                       hipEvent_t after_step = nullptr) {
         if (n > (size_t)INT32_MAX) return fail(FFTCONV_E_UNSUPPORTED, "process length exceeds 2^31-1");
         if (n == 0 || C == 0) return FFTCONV_OK;
         ProcArgs a{};
@@ -612,6 +616,7 @@ struct UniformCore {
                 HIP_TRY(launch_process_la(log2b, a, (int)C, s));
                 la_advance();
             }
+            if (after_step) HIP_TRY(hipEventRecord(after_step, s));
             return FFTCONV_OK;
         }
         if (la_W) la_all = true;  // this launch drops every window
@@ -627,11 +632,13 @@ struct UniformCore {
             a.gw = gwin.p;
             a.gw_t = (int)(gw_t % (unsigned long long)gw_p);
             HIP_TRY(launch_process(log2b, a, (int)C, s));
+            if (after_step) HIP_TRY(hipEventRecord(after_step, s));
             HIP_TRY(launch_gw_anchor(log2b, a, (int)C, s));
             ++gw_t;
             return FFTCONV_OK;
         }
         HIP_TRY(launch_process(log2b, a, (int)C, s));
+        if (after_step) HIP_TRY(hipEventRecord(after_step, s));
         return FFTCONV_OK;
     }
 
@@ -775,13 +782,17 @@ struct TwoStageCore {
     // profiles/r5/r5f_*).  null when `side` is unmasked already.
     hipStream_t side_open = nullptr;
     bool period_runs = false;  // this period's calls went through multi-call launches
-    hipEvent_t ev_main = nullptr, ev_tail = nullptr;
+    // ev_tail: the tail's step (its output, what the next period reads);
+    // ev_tail_done: everything of it, its window anchor included (quiesce)
+    hipEvent_t ev_main = nullptr, ev_tail = nullptr, ev_tail_done = nullptr;
     bool tail_in_flight = false;
     // tail0 deferred to the end of its period (launch_tail0_flush): the
     // aligned calls' blocks [t0_off, t0_off + t0_n * head_bs) of tail_input
     // still to be convolved by tail_convolver0 (FFTCONV_TAIL0_DEFER=0: off)
     bool t0_defer = false;
     mutable size_t t0_off = 0, t0_n = 0;
+    // pending blocks [0, t0_have) whose spectra a run already wrote to t0_xs
+    mutable size_t t0_have = 0;
     size_t t0_nmax = 0;
     DevPtr<float2> t0_xs;
     DevPtr<float> t0_ys;
@@ -800,6 +811,7 @@ struct TwoStageCore {
         if (stream) (void)hipStreamDestroy(stream);
         if (ev_main) (void)hipEventDestroy(ev_main);
         if (ev_tail) (void)hipEventDestroy(ev_tail);
+        if (ev_tail_done) (void)hipEventDestroy(ev_tail_done);
     }
 
     float *tail_input() const { return tin_buf[tin_idx].p; }
@@ -808,7 +820,7 @@ struct TwoStageCore {
     // (StreamOrder) and the tail convolution on the side stream
     int quiesce() const {
         if (int r = order.enter(stream)) return r;
-        if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(stream, ev_tail, 0));
+        if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(stream, ev_tail_done, 0));
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -876,6 +888,7 @@ struct TwoStageCore {
         if (int r = create_side_stream()) return r;
         HIP_TRY(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev_tail_done, hipEventDisableTiming));
         for (auto *b : {&out0, &pre0, &out1, &pre1, &tin_buf[0], &tin_buf[1]}) {
             if (int r = b->alloc(C * T)) return r;
             if (b->n) HIP_TRY(hipMemsetAsync(b->p, 0, b->bytes(), stream));
@@ -895,7 +908,7 @@ struct TwoStageCore {
             if (int r = t0_cv.alloc(C * t0_nmax * head_bs)) return r;
             HIP_TRY(hipMemsetAsync(t0_err.p, 0, t0_err.bytes(), stream));
         }
-        t0_off = t0_n = 0;
+        t0_off = t0_n = t0_have = 0;
         return FFTCONV_OK;
     }
 
@@ -909,8 +922,9 @@ struct TwoStageCore {
         a.xs = t0_xs.p; a.ys = t0_ys.p; a.err = t0_err.p; a.ov0 = t0_ov.p; a.cv = t0_cv.p;
         a.act = (int)tail0->S;
         a.n = (int)t0_n; a.nmax = (int)t0_nmax;
+        a.k0 = (int)std::min(t0_have, t0_n);
         HIP_TRY(launch_tail0_flush(tail0->log2b, a, (int)C, s));
-        t0_n = 0;  // (only once the flush is enqueued: a failed launch keeps the blocks pending)
+        t0_n = t0_have = 0;  // (only once the flush is enqueued: a failed launch keeps the blocks pending)
         return FFTCONV_OK;
     }
 
@@ -989,8 +1003,11 @@ struct TwoStageCore {
             hipStream_t ts = period_runs && side_open ? side_open : side;
             HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
             HIP_TRY(hipStreamWaitEvent(ts, ev_main, 0));
-            if (int r = tail->process_device(tail_input(), T, tail_output, T, T, ts)) return r;
-            HIP_TRY(hipEventRecord(ev_tail, ts));
+            // (the next period waits for the tail's output only, not for its
+            // window anchor: 19 us of cross-queue wait behind the anchor, r5p)
+            if (int r = tail->process_device(tail_input(), T, tail_output, T, T, ts, 0, nullptr, nullptr, ev_tail))
+                return r;
+            HIP_TRY(hipEventRecord(ev_tail_done, ts));
             tail_in_flight = true;
         }
         period_runs = false;
@@ -1090,11 +1107,19 @@ struct TwoStageCore {
                 a.job[0].tin_stride = (long long)T;
                 a.njobs = 1;
                 a.tw = head->tw.p;
+                // the run's block spectra double as tail0's pending-block
+                // spectra while every pending block so far has one
+                const bool t0spec = t0_have == t0_n && t0_n + nrun <= t0_nmax;
+                if (t0spec) {
+                    a.job[0].t0x = t0_xs.p + t0_n * head_bs;
+                    a.job[0].t0x_stride = (long long)(t0_nmax * head_bs);
+                }
                 RunSteps r{(long long)in_step, (long long)out_step, (int)nrun};
                 HIP_TRY(launch_process_run(head->log2b, a, r, (int)C, s));
                 period_runs = true;
                 if (t0_n == 0) t0_off = tail_input_fill;  // :464-472, deferred
                 t0_n += nrun;
+                if (t0spec) t0_have += nrun;
                 precalculated_pos += nrun * len;
                 tail_input_fill += nrun * len;
                 k += nrun;
@@ -1134,7 +1159,7 @@ struct TwoStageCore {
         tail_input_fill = 0;
         precalculated_pos = 0;
         tail_in_flight = false;
-        t0_n = 0;  // (the deferred blocks' state is reset with everything else)
+        t0_n = t0_have = 0;  // (the deferred blocks' state is reset with everything else)
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }

@@ -36,7 +36,9 @@ struct Geo {
     static constexpr int F = B / VEC;                   // slots per row
     static constexpr int G = F >= NT ? 1 : NT / F;      // row groups (segment split)
     static constexpr int SPT = F >= NT ? F / NT : 1;    // slots per thread
-    static constexpr int U = SPT == 1 ? 8 : (SPT == 2 ? 2 : 1);  // rows in flight per thread
+    // rows in flight per thread (B 4096 on 512 threads: 2 rows measured no
+    // faster than 1 -- its near-row MAC streams at the chip's rate, r5o)
+    static constexpr int U = SPT == 1 ? 8 : (SPT == 2 ? 2 : 1);
     static constexpr size_t red_bytes = G > 1 ? (size_t)NT * VEC * sizeof(float2) : 0;
     // B <= 512: the prologue stages by LDS-DMA the twiddle table (2B float2),
     // H[0] (B float2), overlap, and the two tail slices (B floats each)
@@ -424,6 +426,20 @@ __device__ __forceinline__ void proc_stamp(const ProcArgs &a, int k) {
     }
 }
 
+// A multi-call launch's chain state between two calls of one channel
+// (upols_run_kernel, pipelined steps at B <= 256): when the previous call ran
+// the pipelined step without a C2R error (`hot`), the twiddles, H[0], H[1]
+// and the next pre_multiplied are still in LDS, the next call's input block
+// was prefetched into LDS stage[par] by a helper wave, and the overlap is in
+// registers -- the call starts its R2C without a memory round trip.  The
+// same values as the loads it replaces: bit-identical.
+struct RunCarry {
+    int hot;
+    int par;                // stage buffer holding this call's input (hot)
+    const float *next_in;   // the next call's input (null: the run's last call)
+    float ov[4];            // overlap samples of the chain's lanes (B <= 256)
+};
+
 // ---------------------------------------------------------------------------
 // Pipelined full-block step (2 <= B <= 512): the common call -- one whole
 // block from an empty input buffer -- when pre[] already holds
@@ -444,9 +460,9 @@ __device__ __forceinline__ void proc_stamp(const ProcArgs &a, int k) {
 // chain runs its C2R -- the reduction leaves the launch's critical path
 // (cfg3 head timeline, profiles/r3: it ran after the chain, 0.5 of 5.5 us).
 // ---------------------------------------------------------------------------
-template <int LOG2B, int NT, bool NTL>
-__device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob &J, size_t c, int cur, int act,
-                                               int flags, unsigned char *smem) {
+template <int LOG2B, int NT, bool NTL, bool RUN = false>
+__device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob &J, size_t c, int cur, int act,
+                                               int flags, unsigned char *smem, RunCarry *rc = nullptr) {
     using Gm = Geo<LOG2B, NT>;
     constexpr int B = Gm::B, F = B / 2;
     constexpr int RPW = F >= 64 ? 1 : 64 / F, SPL = F >= 64 ? F / 64 : 1;
@@ -487,15 +503,26 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     for (int i = 0; i < CNB; ++i) ovr[i] = p0r[i] = p1r[i] = 0.f;
     float2 *Z = bufA, *Q = bufB;  // (the chain's transform buffers, across B1)
     bool err = false;
+    constexpr bool RH = RUN && Gm::PIPE_EARLY && CNB <= 4;  // (run-carried state: B <= 256)
+    float *stage[2] = {ovl, p0l};  // (a run's prefetched input blocks: LDS the step leaves unused)
+    const bool hot = RH && rc->hot;
     if (wave == 0) {
         // ---- critical chain, one wave: R2C, conv, the C2R error check ----
-        dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);   // x[0..B) as packed z[0..B/2)
-        for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
-        dma_16b<64>(twl, a.tw, 2 * B * (int)sizeof(float2));
-        dma_16b<64>(h0l, Hc, B * (int)sizeof(float2));
-        if (act > 1) dma_16b<64>(h1l, Hc + B, B * (int)sizeof(float2));
-        dma_16b<64>(prel, prec, B * (int)sizeof(float2));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (hot) {
+            // tw, H[0], H[1] and pre in LDS already; the block from the stage
+            const float *sg = stage[rc->par];
+            float *za = reinterpret_cast<float *>(bufA);
+            for (int j = lane; j < B; j += 64) za[j] = sg[j];
+            for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
+        } else {
+            dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);   // x[0..B) as packed z[0..B/2)
+            for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
+            dma_16b<64>(twl, a.tw, 2 * B * (int)sizeof(float2));
+            dma_16b<64>(h0l, Hc, B * (int)sizeof(float2));
+            if (act > 1) dma_16b<64>(h1l, Hc + B, B * (int)sizeof(float2));
+            dma_16b<64>(prel, prec, B * (int)sizeof(float2));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         wave_sync();
         // the overlap and the two-stage adds are read only by the overlap-add
         // at the chain's end: plain loads issued now arrive under the
@@ -505,7 +532,8 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         for (int i = 0; i < CNB; ++i) {
             const int j = lane + 64 * i;
             if (j < B) {
-                ovr[i] = ovc[j];
+                if constexpr (RH) ovr[i] = hot ? rc->ov[i] : ovc[j];
+                else ovr[i] = ovc[j];
                 if (J.add0) p0r[i] = J.add0[c * J.add_stride + j];
                 if (J.add1) p1r[i] = J.add1[c * J.add_stride + j];
             }
@@ -520,10 +548,12 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
         Q = Z == bufA ? bufB : bufA;
         float2 *Xcur = Xc + (size_t)cur * B;
+        float2 *t0r = J.t0x ? J.t0x + c * J.t0x_stride : nullptr;  // (a run: tail0's copy of the spectrum)
         for (int m = lane; m < B; m += 64) {
             const float2 v = real_post<LOG2B, 64>(Z, m, twl);
             Q[m] = v;
             Xcur[m] = v;
+            if (t0r) t0r[m] = v;
         }
         wave_sync();
         bool bad = false;  // conv = pre + X (.) H[0] (:256-261), then the C2R error check
@@ -558,6 +588,8 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         }
     } else if constexpr (Gm::PIPE_EARLY) {
         // ---- helper waves: FDL rows 2..act-1 - w0 of the next block's pre ----
+        // (a run: wave 1 first prefetches the next call's block into the other stage)
+        if (RH && wave == 1 && rc->next_in) dma_f32<64>(stage[rc->par ^ 1], rc->next_in + c * J.in_stride, B);
         const int R = act > 2 ? act - 2 : 0;
         const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
         mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R - w0, NSW, wave - 1, rsub, f0);
@@ -588,6 +620,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
                 }
                 outc[j] = v;
                 ovc[j] = y[B + j] * invN;  // :283-284
+                if constexpr (RH) rc->ov[i] = y[B + j] * invN;
             }
         } else {
             // output.fill(0); return (:264-267): the block stays in the input
@@ -607,7 +640,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
             }
         }
         if (!Gm::PIPE_EARLY && lane == 0) s_err = err ? 1 : 0;
-        if constexpr (Gm::PIPE_EARLY) return;
+        if constexpr (Gm::PIPE_EARLY) return !err;
     }
     if constexpr (Gm::PIPE_EARLY) {
         // ---- helper waves: the next block's pre in its fixed-order
@@ -615,17 +648,20 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
         const int ht = tid - 64;
         if (s_err) {
             if (ht == 0) J.state[c] = make_int4(cur, act, 0, la_clear(flags | FLAG_INBUF, a));
-            return;
+            if constexpr (RH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the stage DMA)
+            return false;
         }
         for (int f = ht; f < F; f += NT - 64) {
             float4 p = red[f];
             for (int w = 0; w <= NSW; ++w)
                 for (int r = (w == 0 ? 1 : 0); r < RPW; ++r) p = vadd(p, red[w * SPL * 64 + f + r * F]);
             reinterpret_cast<float4 *>(prec)[f] = p;
+            if constexpr (RH) reinterpret_cast<float4 *>(prel)[f] = p;  // (the chain's C2R no longer reads prel)
         }
         if (ht == 0) J.state[c] = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
+        if constexpr (RH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the stage DMA has landed)
         proc_stamp(a, 3);
-        return;
+        return true;
     }
     // ---- FDL rows 2..act-1 of the next block's pre: waves 1..NSW take
     // t in [0, R0), wave 0 (after its chain) the last w0 rows ----
@@ -640,7 +676,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     __syncthreads();
     if (s_err) {
         if (tid == 0) J.state[c] = make_int4(cur, act, 0, la_clear(flags | FLAG_INBUF, a));
-        return;
+        return false;
     }
     // next block's pre: every lane parks its partial sums in LDS (the whole
     // workgroup's staging is dead now), then slot f sums waves 0..NSW and
@@ -657,6 +693,7 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
     }
     if (tid == 0) J.state[c] = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
     proc_stamp(a, 3);
+    return false;  // (B = 512: no run-carried state)
 }
 
 // ---------------------------------------------------------------------------
@@ -669,9 +706,11 @@ __device__ __forceinline__ void pipelined_step(const ProcArgs &a, const ProcJob 
 // the overlap and the two-stage tail slices.  After the MAC the FFT / C2R /
 // overlap-add tail then runs out of LDS and registers only.
 // ---------------------------------------------------------------------------
-template <int LOG2B, int NT, bool ZZ, bool NTL>
-__device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J, const size_t c, const int4 st,
-                                            unsigned char *smem) {
+// returns true when the call ran the pipelined step without a C2R error and
+// left a multi-call launch's chain state in LDS (RunCarry::hot)
+template <int LOG2B, int NT, bool ZZ, bool NTL, bool RUN = false>
+__device__ __forceinline__ bool process_job(const ProcArgs &a, const ProcJob &J, const size_t c, const int4 st,
+                                            unsigned char *smem, RunCarry *rc = nullptr) {
     using Gm = Geo<LOG2B, NT>;
     constexpr int B = Gm::B, VEC = Gm::VEC, F = Gm::F, G = Gm::G, SPT = Gm::SPT;
     constexpr float invN = 1.0f / (float)(2 * B);
@@ -694,14 +733,12 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
     if (act == 0) {  // :216-219 -- zero output, state untouched
         for (int j = tid; j < n; j += NT) outc[j] = 0.f;
         twostage_epilogue<NT>(J, c, outc, inc, n);
-        return;
+        return false;
     }
 
     if constexpr (Gm::PIPE) {
-        if (a.pipe && fill == 0 && n == B && !(flags & FLAG_INBUF) && (flags & FLAG_PRE) && cur < act && !ZZ) {
-            pipelined_step<LOG2B, NT, NTL>(a, J, c, cur, act, flags, smem);
-            return;
-        }
+        if (a.pipe && fill == 0 && n == B && !(flags & FLAG_INBUF) && (flags & FLAG_PRE) && cur < act && !ZZ)
+            return pipelined_step<LOG2B, NT, NTL, RUN>(a, J, c, cur, act, flags, smem, rc);
     }
 
     const size_t rows = (size_t)J.S * B;
@@ -854,10 +891,13 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
         float2 *Z = lds_cfft<LOG2B, NT, false>(bufA, bufB, tw);
         float2 *Q = Z == bufA ? bufB : bufA;
         float2 *Xcur = Xc + (size_t)cur * B;
+        // (a run's two-stage head: tail0's copy of a whole block's spectrum)
+        float2 *t0r = J.t0x && fill == 0 && k == B ? J.t0x + c * J.t0x_stride : nullptr;
         for (int m = tid; m < B; m += NT) {
             const float2 v = real_post<LOG2B, NT>(Z, m, tw);
             Q[m] = v;
             Xcur[m] = v;
+            if (t0r) t0r[m] = v;
         }
         __syncthreads();
         proc_stamp(a, 1);  // (R2C done)
@@ -937,6 +977,7 @@ __device__ __forceinline__ void process_job(const ProcArgs &a, const ProcJob &J,
     if (tid == 0) J.state[c] = make_int4(cur, act, fill, la_clear(flags, a) | (gwin && !err ? FLAG_GW : 0));
     if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
     proc_stamp(a, 3);
+    return false;
 }
 
 // ---------------------------------------------------------------------------
@@ -1046,14 +1087,19 @@ __global__ __launch_bounds__(NT, 2) void upols_run_kernel(ProcArgs a, RunSteps r
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const size_t c = blockIdx.x;
     ProcJob J = a.job[0];
+    RunCarry rc{};
     for (int k = 0; k < r.n; ++k) {
-        process_job<LOG2B, NT, false, NTL>(a, J, c, J.state[c], smem);
+        rc.next_in = k + 1 < r.n ? J.in + r.in_step : nullptr;
+        const bool kept = process_job<LOG2B, NT, false, NTL, true>(a, J, c, J.state[c], smem, &rc);
+        rc.hot = kept && rc.next_in != nullptr;  // (the next call's block is in stage[par ^ 1])
+        rc.par ^= 1;
         __syncthreads();
         J.in += r.in_step;
         J.out += r.out_step;
         if (J.add0) J.add0 += J.n;
         if (J.add1) J.add1 += J.n;
         if (J.tin) J.tin += J.n;
+        if (J.t0x) J.t0x += J.n;
     }
 }
 
@@ -1662,7 +1708,7 @@ __global__ __launch_bounds__(64) void tail0_r2c_kernel(Tail0Args t) {
     float2 *bufA = reinterpret_cast<float2 *>(smem), *bufB = bufA + B, *twl = bufB + B;
     const ProcJob &J = t.pa.job[0];
     const size_t c = blockIdx.x;
-    const int k = blockIdx.y, lane = threadIdx.x;
+    const int k = t.k0 + (int)blockIdx.y, lane = threadIdx.x;
     dma_f32<64>(reinterpret_cast<float *>(bufA), J.in + c * J.in_stride + (size_t)k * B, B);  // packed z[0..B/2)
     for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);              // the padding half
     dma_16b<64>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
@@ -1671,7 +1717,7 @@ __global__ __launch_bounds__(64) void tail0_r2c_kernel(Tail0Args t) {
     float2 *Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);
     float2 *xr = t.xs + ((size_t)c * t.nmax + k) * B;
     for (int m = lane; m < B; m += 64) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
-    if (k == 0) {  // the overlap before the period's blocks, for (3) (whose tiles overwrite it)
+    if (k == 0) {  // the overlap before the period's blocks, for (3) (whose tiles overwrite it; k0 = 0)
         for (int j = lane; j < B; j += 64) t.ov0[c * B + j] = J.overlap[c * B + j];
     }
 }
@@ -2220,7 +2266,19 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
                 return hipGetLastError();
             }
         }
-        hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
+        // (blocks [0, k0) have their spectra from the head's run; the overlap
+        // copy tail0_r2c makes at block 0 is then made here)
+        if (t.k0 < 0 || t.k0 > a.n) return hipErrorInvalidValue;
+        if (t.k0 > 0) {
+            const ProcJob &J = t.pa.job[0];
+            if (hipError_t e = hipMemcpyAsync(t.ov0, J.overlap, (size_t)channels * B * sizeof(float),
+                                              hipMemcpyDeviceToDevice, s);
+                e != hipSuccess)
+                return e;
+        }
+        if (t.k0 < a.n)
+            hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n - t.k0), dim3(64), 4 * B * sizeof(float2),
+                               s, t);
         hipLaunchKernelGGL(mk, dim3(channels, F / FC), dim3(256), lds, s, t);
         hipLaunchKernelGGL(tail0_c2r_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
         hipLaunchKernelGGL(tail0_commit_kernel<LOG2B>, dim3(channels, (a.n + KT - 1) / KT), dim3(256), 0, s, t);

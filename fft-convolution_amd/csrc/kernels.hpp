@@ -105,6 +105,12 @@ struct ProcJob {
     // [C][B] scratch between the row and the column passes of the inverse
     int4 *lg_prog;
     float2 *lg_v;
+    // two-stage head of a multi-call launch (upols_run_kernel): its block's
+    // spectrum also goes to the deferred tail0's pending-block row
+    // t0x + c * t0x_stride (the same R2C tail0_r2c_kernel would compute), so
+    // the period's flush skips those blocks' transforms; null = none
+    float2 *t0x;
+    long long t0x_stride;
 };
 
 // Twiddle tables of the long-block path (large.hip), f64-rounded f32:
@@ -289,6 +295,7 @@ struct Tail0Args {
     int act;               // tail0's active segments (every channel: TwoStage never updates tail0)
     int n;                 // pending blocks
     int nmax;              // row pitch of xs / ys in blocks
+    int k0;                // blocks [0, k0) already have their spectra in xs (the head's run wrote them)
 };
 bool tail0_defer_supported(int log2b, int act, int nmax);
 bool tail0_defer_allowed();  // VARIANT_T0BLOCK unset
