@@ -1481,7 +1481,10 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
 //    wave needs one B-point buffer and a workgroup runs IR_NW = 8 waves --
 //    twice the segment loads in flight per CU of the ping-pong layout.
 // grid (ceil(S / (NW * IR_SPW)), channels); LDS: tw (2B) | NW x bufA (| bufB: B < 128)
-constexpr int IR_SPW = 2;
+#ifndef FFTCONV_IR_SPW
+#define FFTCONV_IR_SPW 2
+#endif
+constexpr int IR_SPW = FFTCONV_IR_SPW;
 template <int LOG2B>
 constexpr int ir_nw() { return LOG2B >= 7 ? 8 : 4; }
 template <int LOG2B>
@@ -1744,6 +1747,11 @@ __global__ __launch_bounds__(256) void tail0_mac_kernel(Tail0Args t) {
     const int tid = threadIdx.x, fl = tid % FC, g = tid / FC;
     const int4 st = J0.state[c];
     const int cur0 = st.x, act = st.y, n = t.n;
+    if (t.k0 > 0 && blockIdx.y == 0) {
+        // the overlap before the period's blocks, for (3) (tail0_r2c copies it
+        // at block 0; with k0 > 0 the head's run made block 0's spectrum)
+        for (int j = tid; j < B; j += 256) t.ov0[c * B + j] = J0.overlap[c * B + j];
+    }
     if (act != t.act) {  // (not a geometry the LDS was sized for: the replay path runs it)
         if (tid == 0) t.err[c] = 1;
         return;
@@ -2267,15 +2275,8 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
             }
         }
         // (blocks [0, k0) have their spectra from the head's run; the overlap
-        // copy tail0_r2c makes at block 0 is then made here)
+        // copy tail0_r2c makes at block 0 is then tail0_mac's)
         if (t.k0 < 0 || t.k0 > a.n) return hipErrorInvalidValue;
-        if (t.k0 > 0) {
-            const ProcJob &J = t.pa.job[0];
-            if (hipError_t e = hipMemcpyAsync(t.ov0, J.overlap, (size_t)channels * B * sizeof(float),
-                                              hipMemcpyDeviceToDevice, s);
-                e != hipSuccess)
-                return e;
-        }
         if (t.k0 < a.n)
             hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n - t.k0), dim3(64), 4 * B * sizeof(float2),
                                s, t);
