@@ -782,6 +782,7 @@ struct TwoStageCore {
     // profiles/r5/r5f_*).  null when `side` is unmasked already.
     hipStream_t side_open = nullptr;
     bool period_runs = false;  // this period's calls went through multi-call launches
+    hipStream_t last_ts = nullptr;  // the side stream of the last tail
     // ev_tail: the tail's step (its output, what the next period reads);
     // ev_tail_done: everything of it, its window anchor included (quiesce)
     hipEvent_t ev_main = nullptr, ev_tail = nullptr, ev_tail_done = nullptr;
@@ -999,16 +1000,21 @@ struct TwoStageCore {
         // the previous period's tail result, so wait for that kernel here
         if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(s, ev_tail, 0));
         if (tail) {                                                            // :484-485
-            // (the previous tail, on either side stream, finished before ev_main)
             hipStream_t ts = period_runs && side_open ? side_open : side;
             HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
             HIP_TRY(hipStreamWaitEvent(ts, ev_main, 0));
+            // ev_main follows the previous tail's step only (ev_tail): its
+            // window anchor ran on its own side stream, so a tail on the other
+            // one starts after that too
+            if (tail_in_flight && ts != last_ts) HIP_TRY(hipStreamWaitEvent(ts, ev_tail_done, 0));
             // (the next period waits for the tail's output only, not for its
-            // window anchor: 19 us of cross-queue wait behind the anchor, r5p)
+            // window anchor: 19 us of cross-queue wait behind the anchor, r5p;
+            // starting the tail before the flush gained nothing, r5s)
             if (int r = tail->process_device(tail_input(), T, tail_output, T, T, ts, 0, nullptr, nullptr, ev_tail))
                 return r;
             HIP_TRY(hipEventRecord(ev_tail_done, ts));
             tail_in_flight = true;
+            last_ts = ts;
         }
         period_runs = false;
         tin_idx ^= 1;  // the next period fills the other buffer while the tail reads this one
