@@ -1020,28 +1020,67 @@ __global__ __launch_bounds__(256) void gw_anchor_kernel(ProcArgs a) {
         DBG_CHECK((cur + o) % act < J.S, 41, cur, o, act, J.S);
         xr[o] = ntld4(X4 + (size_t)((cur + o) % act) * F);
     }
+    // P rows in flight; on the long-block path (one wave per SIMD: latency is
+    // not hidden by other waves) software-pipelined: the next P rows' loads
+    // are issued before this batch's MACs.  (The two-stage tail's anchor at
+    // B <= 8192 runs beside the head on few CUs: the plain loop's lower
+    // register count measured faster there.)
     int i0 = P;
-    for (; i0 + P <= act; i0 += P) {  // P rows in flight
+    if constexpr (LOG2B > kMaxLog2Fused) {
         float4 h[P], xn[P];
+        if (i0 + P <= act) {
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
-            xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
+            for (int j = 0; j < P; ++j) {
+                h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
+                xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
+            }
         }
+        for (; i0 + P <= act; i0 += P) {
+            float4 h2[P], x2[P];
+            const bool more = i0 + 2 * P <= act;
+            if (more) {
 #pragma unroll
-        for (int j = 0; j < P; ++j)
+                for (int j = 0; j < P; ++j) {
+                    h2[j] = ntld4(H4 + (size_t)(i0 + P + j) * F);
+                    x2[j] = ntld4(X4 + (size_t)((cur + i0 + P + j) % act) * F);
+                }
+            }
 #pragma unroll
-            for (int k = 0; k < P; ++k) w[k].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
+            for (int j = 0; j < P; ++j)
 #pragma unroll
-        for (int j = 0; j < P; ++j) xr[j] = xn[j];
+                for (int k = 0; k < P; ++k) w[k].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                xr[j] = xn[j];
+                if (more) {
+                    h[j] = h2[j];
+                    xn[j] = x2[j];
+                }
+            }
+        }
+    } else {
+        for (; i0 + P <= act; i0 += P) {
+            float4 h[P], xn[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
+                xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
+            }
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int k = 0; k < P; ++k) w[k].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
+#pragma unroll
+            for (int j = 0; j < P; ++j) xr[j] = xn[j];
+        }
     }
 #pragma unroll
     for (int j = 0; j < P; ++j) {
         if (i0 + j < act) {
-            const float4 h = ntld4(H4 + (size_t)(i0 + j) * F);
+            const float4 hv = ntld4(H4 + (size_t)(i0 + j) * F);
             xr[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
 #pragma unroll
-            for (int k = 0; k < P; ++k) w[k].mac(h, xr[(j - k + P) % P]);
+            for (int k = 0; k < P; ++k) w[k].mac(hv, xr[(j - k + P) % P]);
         }
     }
     float4 *W4 = reinterpret_cast<float4 *>(a.gw + (size_t)c * P * B) + f;
@@ -2173,11 +2212,20 @@ hipError_t launch_gw_anchor(int log2b, const ProcArgs &a, int channels, hipStrea
         case 11: return launch_gw_anchor_t<11>(a, channels, s);
         case 12: return launch_gw_anchor_t<12>(a, channels, s);
         case 13: return launch_gw_anchor_t<13>(a, channels, s);
+        case 14: return launch_gw_anchor_t<14>(a, channels, s);
+        case 15: return launch_gw_anchor_t<15>(a, channels, s);
+        case 16: return launch_gw_anchor_t<16>(a, channels, s);
+        case 17: return launch_gw_anchor_t<17>(a, channels, s);
+        case 18: return launch_gw_anchor_t<18>(a, channels, s);
+        case 19: return launch_gw_anchor_t<19>(a, channels, s);
+        case 20: return launch_gw_anchor_t<20>(a, channels, s);
+        case 21: return launch_gw_anchor_t<21>(a, channels, s);
+        case 22: return launch_gw_anchor_t<22>(a, channels, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-bool gw_supported(int log2b, int S) { return log2b >= 10 && log2b <= kMaxLog2Fused && S >= 3 * kGwP; }
+bool gw_supported(int log2b, int S) { return log2b >= 10 && log2b <= kMaxLog2Block && S >= 3 * kGwP; }
 
 template <int LOG2B>
 static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t s) {

@@ -45,21 +45,30 @@ namespace fftconv {
 namespace {
 
 constexpr int LG_NT = 256;
-constexpr int LG_E = 4096;  // complex points per column tile (passes A and C)
+constexpr int LG_E = 4096;  // complex points per column tile (passes A and C), at most
+// tiles per transform, at least (A/B builds: 8 or 16 tiles at B = 16384 --
+// 128..256-byte column runs -- measured 2-20% slower than 4 tiles of 512-byte
+// runs, profiles/r5/r5y_ab_lg_tiles.log)
+#ifndef FFTCONV_LG_TILES
+#define FFTCONV_LG_TILES 1
+#endif
 
 template <int LM>
 struct LgGeo {
     static constexpr int L2 = LM - 6 < 11 ? LM - 6 : 11;  // row length M2 = 2^L2 (256..2048)
     static constexpr int L1 = LM - L2;                     // column length M1 = 2^L1 (64..2048)
     static constexpr int M = 1 << LM, M1 = 1 << L1, M2 = 1 << L2;
-    static constexpr int TC = LG_E / M1;                   // columns per pass-A / pass-C tile
+    // complex points per pass-A / pass-C tile: LG_E, or fewer for FFTCONV_LG_TILES tiles (>= 2 columns)
+    static constexpr int E0 = M / FFTCONV_LG_TILES < LG_E ? M / FFTCONV_LG_TILES : LG_E;
+    static constexpr int E = E0 > 2 * M1 ? E0 : 2 * M1;
+    static constexpr int TC = E / M1;                      // columns per pass-A / pass-C tile
     static constexpr int NTILE = M2 / TC;                  // tiles per row of the [M1][M2] array
     static constexpr int NPAIR = M1 / 2;                   // pass-B workgroups per transform
     static constexpr int EP = 2 * M2 / (2 * LG_NT);        // pass B: element pairs per thread
-    static constexpr size_t col_lds = 2 * (size_t)LG_E * sizeof(float2);
+    static constexpr size_t col_lds = 2 * (size_t)E * sizeof(float2);
     static constexpr size_t row_lds = 2 * 2 * (size_t)M2 * sizeof(float2);
     static_assert(LM >= 14 && LM <= 22, "long-block path: 2^14 <= B <= 2^22");
-    static_assert(TC >= 2 && TC <= M2 && EP >= 1, "tile shape");
+    static_assert(TC >= 2 && TC <= M2 && EP >= 1 && E % LG_NT == 0 && E <= LG_E, "tile shape");
 };
 
 // ---------------------------------------------------------------------------
@@ -150,6 +159,7 @@ __device__ __forceinline__ float4 mac4(float4 acc, float4 h, float4 x, bool slot
     r.w = fmaf(h.w, x.z, fmaf(h.z, x.w, acc.w));
     return r;
 }
+__device__ __forceinline__ float4 vadd4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 
 // one channel's chunk of the reference's chunk loop (:222-232), from its
 // block state and the call's progress word {processed, done, c2r failed,
@@ -192,7 +202,21 @@ struct LgPass {
     int *status;
     float2 *Y;              // [rows][M] scratch
     int row0;               // first row of this batch
+    // LG_CONV far-row windows (ProcArgs::gw_p / gw / gw_t)
+    const float2 *gw;
+    int gw_p, gw_t;
 };
+
+// the far-row split of a channel's pre_multiplied (0 = one sum) and whether
+// this chunk reads its window row: the generic step's rule (kernels.hip
+// process_job) -- a one-block call from an empty input buffer, window live
+__device__ __forceinline__ int lg_split(const LgPass &p, const Chunk &ch) {
+    return p.gw_p > 0 && ch.act > p.gw_p ? p.gw_p : 0;
+}
+__device__ __forceinline__ bool lg_window(const LgPass &p, const Chunk &ch, int sp, int B) {
+    return sp && p.gw && ch.fill == 0 && ch.processed == 0 && p.J.n == B &&
+           !(ch.flags & (FLAG_INBUF | FLAG_PRE)) && (ch.flags & FLAG_GW);
+}
 
 // ---------------------------------------------------------------------------
 // pass A: packed input -> column FFTs -> x W_M^(n2 k1) -> rows of Y
@@ -204,7 +228,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
     using G = LgGeo<LM>;
     constexpr int M = G::M, M1 = G::M1, M2 = G::M2, TC = G::TC;
     extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
-    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + LG_E;
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + G::E;
     const int tid = threadIdx.x;
     const int tile = blockIdx.x % G::NTILE;
     const size_t row = blockIdx.x / G::NTILE;
@@ -226,7 +250,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
             if (i >= ch.fill && i < ch.fill + ch.k) return inc[ch.processed + i - ch.fill];
             return inb ? ibc[i] : 0.f;
         };
-        for (int e = tid; e < LG_E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = n1 < M1 / 2 ? make_float2(x(2 * n), x(2 * n + 1)) : make_float2(0.f, 0.f);
@@ -238,7 +262,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
         const float *src = p.src + ch * p.src_stride;
         const long long base = (long long)s * M;  // (B = M samples per segment)
         auto x = [&](int i) -> float { return base + i < p.len_data ? src[base + i] : 0.f; };
-        for (int e = tid; e < LG_E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = n1 < M1 / 2 ? make_float2(x(2 * n), x(2 * n + 1)) : make_float2(0.f, 0.f);
@@ -246,7 +270,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
     } else {
         Y = p.Y + row * M;
         const float *in = p.in + (p.row0 + row) * p.in_stride;
-        for (int e = tid; e < LG_E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = make_float2(in[2 * n], in[2 * n + 1]);
@@ -254,7 +278,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
     }
     __syncthreads();
     const float2 *R = bfft<G::L1, TC, true, false>(b0, b1, p.tb.twA, tid);
-    for (int e = tid; e < LG_E; e += LG_NT) {
+    for (int e = tid; e < G::E; e += LG_NT) {
         const int t = e & (TC - 1), k1 = e / TC;
         const int n2 = c0 + t;
         DBG_CHECK(k1 < M1 && n2 < M2, 52, k1, n2, tile, (int)row);  // (site 52: pass A's Y position)
@@ -381,11 +405,6 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
         }
         if (ch.fill == 0) {
             // pre_multiplied = sum_{i=1}^{act-1} H[i] (.) X[(current + i) % act] (:244-255)
-#pragma unroll
-            for (int u = 0; u < EP; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            // RU rows in flight per thread (RU x EP x 2 float4 loads issued
-            // before their MACs), then the MACs in row order: the same sums
-            // in the same order as one row at a time
 #ifdef FFTCONV_LG_RU
             constexpr int RU = FFTCONV_LG_RU;  // (A/B builds)
 #else
@@ -397,40 +416,67 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
             const float4 *H4 = reinterpret_cast<const float4 *>(Hc);
             const float4 *X4 = reinterpret_cast<const float4 *>(Xc);
             constexpr size_t RF = (size_t)M / 2;  // float4 per row
-            int xi = (ch.cur + 1) % ch.act;  // (current may exceed act after an update shrank it)
-            int i = 1;
-            for (; i + RU <= ch.act; i += RU) {
-                float4 hv[RU][EP], xv[RU][EP];
-                int xr = xi;
+            // rows [i0, i1) summed from zero into r: RU rows in flight per
+            // thread (RU x EP x 2 float4 loads issued before their MACs), then
+            // the MACs in row order -- the same sums in the same order as one
+            // row at a time
+            auto mac_range = [&](float4 (&r)[EP], int i0, int i1) {
 #pragma unroll
-                for (int r = 0; r < RU; ++r) {
+                for (int u = 0; u < EP; ++u) r[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                int xi = (ch.cur + i0) % ch.act;  // (current may exceed act after an update shrank it)
+                int i = i0;
+                for (; i + RU <= i1; i += RU) {
+                    float4 hv[RU][EP], xv[RU][EP];
+                    int xr = xi;
+#pragma unroll
+                    for (int t = 0; t < RU; ++t) {
+#pragma unroll
+                        for (int u = 0; u < EP; ++u) {
+                            DBG_CHECK(xr >= 0 && xr < ch.act && 2 * q[u] + 1 < (size_t)M, 54, xr, ch.act, (int)q[u],
+                                      i + t);  // (site 54: a MAC row)
+                            hv[t][u] = ntload(H4 + (size_t)(i + t) * RF + q[u]);
+                            xv[t][u] = ntload(X4 + (size_t)xr * RF + q[u]);
+                        }
+                        if (++xr == ch.act) xr = 0;
+                    }
+#pragma unroll
+                    for (int t = 0; t < RU; ++t)
+#pragma unroll
+                        for (int u = 0; u < EP; ++u)
+                            r[u] = mac4(r[u], hv[t][u], xv[t][u], tid == 0 && u == 0 && rp.w == 0);
+                    xi = xr;
+                }
+                for (; i < i1; ++i) {
+                    float4 hv[EP], xv[EP];
 #pragma unroll
                     for (int u = 0; u < EP; ++u) {
-                        DBG_CHECK(xr >= 0 && xr < ch.act && 2 * q[u] + 1 < (size_t)M, 54, xr, ch.act, (int)q[u],
-                                  i + r);  // (site 54: a MAC row)
-                        hv[r][u] = ntload(H4 + (size_t)(i + r) * RF + q[u]);
-                        xv[r][u] = ntload(X4 + (size_t)xr * RF + q[u]);
+                        DBG_CHECK(xi >= 0 && xi < ch.act, 54, xi, ch.act, (int)q[u], i);
+                        hv[u] = ntload(H4 + (size_t)i * RF + q[u]);
+                        xv[u] = ntload(X4 + (size_t)xi * RF + q[u]);
                     }
-                    if (++xr == ch.act) xr = 0;
+#pragma unroll
+                    for (int u = 0; u < EP; ++u) r[u] = mac4(r[u], hv[u], xv[u], tid == 0 && u == 0 && rp.w == 0);
+                    if (++xi == ch.act) xi = 0;
                 }
+            };
+            // far-row windows (as the generic step): rows 1..sp-1
+            // plus rows sp..act-1 in every launch of such a batch; a one-block
+            // call of a channel whose window is live reads the far part from
+            // its window row (gw_anchor_kernel summed it with the same
+            // arithmetic), else sums it here
+            const int sp = lg_split(p, ch);
+            mac_range(acc, 1, sp ? sp : ch.act);
+            if (lg_window(p, ch, sp, M)) {
+                const int k = (int)(((long long)p.gw_t - 1 - (long long)row) % sp + sp) % sp;
+                DBG_CHECK(k >= 0 && k < sp, 60, k, p.gw_t, sp, (int)row);  // (site 60: the window row)
+                const float4 *wr = reinterpret_cast<const float4 *>(p.gw + (row * sp + k) * (size_t)M);
 #pragma unroll
-                for (int r = 0; r < RU; ++r)
+                for (int u = 0; u < EP; ++u) acc[u] = vadd4(acc[u], ntload(wr + q[u]));
+            } else if (sp) {
+                float4 far[EP];
+                mac_range(far, sp, ch.act);
 #pragma unroll
-                    for (int u = 0; u < EP; ++u)
-                        acc[u] = mac4(acc[u], hv[r][u], xv[r][u], tid == 0 && u == 0 && rp.w == 0);
-                xi = xr;
-            }
-            for (; i < ch.act; ++i) {
-                float4 hv[EP], xv[EP];
-#pragma unroll
-                for (int u = 0; u < EP; ++u) {
-                    DBG_CHECK(xi >= 0 && xi < ch.act, 54, xi, ch.act, (int)q[u], i);
-                    hv[u] = ntload(H4 + (size_t)i * RF + q[u]);
-                    xv[u] = ntload(X4 + (size_t)xi * RF + q[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < EP; ++u) acc[u] = mac4(acc[u], hv[u], xv[u], tid == 0 && u == 0 && rp.w == 0);
-                if (++xi == ch.act) xi = 0;
+                for (int u = 0; u < EP; ++u) acc[u] = vadd4(acc[u], far[u]);
             }
 #pragma unroll
             for (int u = 0; u < EP; ++u)
@@ -506,7 +552,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
     constexpr int M = G::M, M2 = G::M2, TC = G::TC, B = M;
     constexpr float invN = 1.0f / (float)(2 * M);
     extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
-    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + LG_E;
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + G::E;
     const int tid = threadIdx.x;
     const int tile = blockIdx.x % G::NTILE;
     const size_t row = blockIdx.x / G::NTILE;
@@ -520,7 +566,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
     } else {
         V = p.Y + row * M;
     }
-    for (int e = tid; e < LG_E; e += LG_NT) {
+    for (int e = tid; e < G::E; e += LG_NT) {
         const int t = e & (TC - 1), k1 = e / TC;
         b0[e] = V[(size_t)k1 * M2 + c0 + t];
     }
@@ -531,7 +577,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
         const float *in = p.in + (p.row0 + row) * p.in_stride;
         const float sc = (in[1] != 0.f || in[2 * M + 1] != 0.f) ? 1.0f : invN;  // (flagged rows stay unscaled)
         float *o = p.out + (p.row0 + row) * p.out_stride;
-        for (int e = tid; e < LG_E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const size_t n = (size_t)n1 * M2 + c0 + t;
             o[2 * n] = R[e].x * sc;
@@ -549,7 +595,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
         const int lo = ch.fill, hi = ch.fill + ch.k;
         const bool complete = hi == B;
         // the first half of the tile's rows (n1 < M1/2) holds samples j < B
-        for (int e = tid; e < LG_E / 2; e += LG_NT) {
+        for (int e = tid; e < G::E / 2; e += LG_NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int j0 = 2 * (n1 * M2 + c0 + t);
 #pragma unroll
@@ -572,7 +618,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
         }
         if (complete && !err) {
             __syncthreads();  // every overlap read above is done (sample j and j + B share the column)
-            for (int e = LG_E / 2 + tid; e < LG_E; e += LG_NT) {
+            for (int e = G::E / 2 + tid; e < G::E; e += LG_NT) {
                 const int t = e & (TC - 1), n1 = e / TC;
                 const int j = 2 * (n1 * M2 + c0 + t) - B;
                 ovc[j] = R[e].x * invN;  // :283-284
@@ -588,6 +634,9 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
             if (old == G::NTILE - 1) {
                 pg[3] = 0;
                 int cur = ch.cur, fill = ch.fill, flags = ch.flags & ~(LA_MASK | SEQ_MASK | FLAG_PRE);
+                // a step that read its window keeps it live for the window's
+                // next block (the generic step's rule)
+                const bool gwin = lg_window(p, ch, lg_split(p, ch), B);
                 if (err) {
                     flags |= FLAG_INBUF;  // fill / current unchanged
                     pg[1] = 1;
@@ -597,6 +646,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
                         flags ^= FLAG_REV;
                         fill = 0;
                         cur = cur > 0 ? cur - 1 : ch.act - 1;  // :287-291
+                        if (gwin) flags |= FLAG_GW;
                     } else {
                         flags |= FLAG_INBUF;
                         fill += ch.k;
@@ -667,6 +717,9 @@ hipError_t lg_process_t(const ProcArgs &a, const LgTab &t, int chunks, int chann
         LgPass p{};
         p.J = a.job[j];
         p.tb = t;
+        p.gw = a.gw;
+        p.gw_p = a.gw_p;
+        p.gw_t = a.gw_t;
         if (!p.J.lg_prog || !p.J.lg_v) return hipErrorInvalidValue;
         if (p.J.n <= 0) continue;
         if (hipError_t e = lds_attr(lg_rows<LM, LG_CONV>, G::row_lds); e != hipSuccess) return e;
@@ -830,18 +883,18 @@ __global__ __launch_bounds__(LG_NT) void bs_cols_fwd(BsPass p) {
     using G = LgGeo<LP>;
     constexpr int M2 = G::M2, TC = G::TC, P = G::M;
     extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
-    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + LG_E;
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + G::E;
     const int tid = threadIdx.x, c0 = (int)(blockIdx.x % G::NTILE) * TC;
     const size_t row = blockIdx.x / G::NTILE;
     const float *in = p.in + (p.row0 + row) * p.in_stride;
-    for (int e = tid; e < LG_E; e += LG_NT) {
+    for (int e = tid; e < G::E; e += LG_NT) {
         const int j = (e / TC) * M2 + c0 + (e & (TC - 1));
         b0[e] = j < p.n ? cmulc(bs_src(p, in, j), p.w[j]) : make_float2(0.f, 0.f);
     }
     __syncthreads();
     const float2 *R = bfft<G::L1, TC, true, false>(b0, b1, p.tb.twA, tid);
     float2 *Y = p.Y + row * P;
-    for (int e = tid; e < LG_E; e += LG_NT) {
+    for (int e = tid; e < G::E; e += LG_NT) {
         const int t = e & (TC - 1), k1 = e / TC, n2 = c0 + t;
         Y[(size_t)k1 * M2 + n2] = cmul(R[e], p.tb.twM[(n2 * k1) & (P - 1)]);
     }
@@ -878,11 +931,11 @@ __global__ __launch_bounds__(LG_NT) void bs_cols_inv(BsPass p) {
     constexpr int M2 = G::M2, TC = G::TC, P = G::M;
     constexpr float invP = 1.0f / (float)P;
     extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
-    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + LG_E;
+    float2 *b0 = reinterpret_cast<float2 *>(lg_smem), *b1 = b0 + G::E;
     const int tid = threadIdx.x, c0 = (int)(blockIdx.x % G::NTILE) * TC;
     const size_t row = blockIdx.x / G::NTILE;
     const float2 *V = p.Y + row * P;
-    for (int e = tid; e < LG_E; e += LG_NT) b0[e] = V[(size_t)(e / TC) * M2 + c0 + (e & (TC - 1))];
+    for (int e = tid; e < G::E; e += LG_NT) b0[e] = V[(size_t)(e / TC) * M2 + c0 + (e & (TC - 1))];
     __syncthreads();
     const float2 *R = bfft<G::L1, TC, true, true>(b0, b1, p.tb.twA, tid);
     const size_t r = p.row0 + row;
@@ -890,7 +943,7 @@ __global__ __launch_bounds__(LG_NT) void bs_cols_inv(BsPass p) {
     const bool flagged = bs_flagged(p, in);
     if (p.status && blockIdx.x % G::NTILE == 0 && tid == 0) p.status[r] = flagged ? 1 : 0;
     float *o = p.out + r * p.out_stride;
-    for (int e = tid; e < LG_E; e += LG_NT) {
+    for (int e = tid; e < G::E; e += LG_NT) {
         const int m = (e / TC) * M2 + c0 + (e & (TC - 1));
         if (m < p.n) bs_out(p, o, m, R[e], invP, flagged);
     }

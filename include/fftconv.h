@@ -113,7 +113,7 @@ int fftconv_fft_inverse_host(int device, size_t n, size_t rows, const float *inp
  * per head block (by default its blocks are convolved together at the end
  * of each tail period; read when a TwoStageFFTConvolver is created), bit 9 =
  * that end-of-period flush in one fused kernel instead of five (head block
- * 64; bit-identical), bit 10 = no far-row windows for 1024 <= B <= 8192 (every
+ * 64; bit-identical), bit 10 = no far-row windows for B >= 1024 (every
  * one-block call sums its far rows itself; bit-identical), bit 11 =
  * process_device_steps launches once per call (by default, for 64 <= B <= 512,
  * a TwoStageFFTConvolver's aligned calls inside one tail period, and the
@@ -203,7 +203,7 @@ size_t fftconv_uniform_channels(const fftconv_uniform *h);
 /* anchor workgroups per channel of the lookahead step, 0 = not used */
 int fftconv_uniform_lookahead_parts(const fftconv_uniform *h);
 /* window rows per channel of the generic step's far-row windows (automatic
- * for standalone batches with 1024 <= B <= 8192 and >= 24 segments: an
+ * for standalone batches with B >= 1024 and >= 24 segments: an
  * anchor every P blocks sums rows >= P for a channel's next P one-block
  * calls; bit-identical to summing them every block), 0 = not used */
 int fftconv_uniform_far_windows(const fftconv_uniform *h);

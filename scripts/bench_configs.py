@@ -75,13 +75,14 @@ def windowed_bytes(B, L, P=GW_P):
     return row * (2 * P + 1) + row * (2 * S - 1) / P + 16 * B
 
 
-def lg_step_bytes(B, L):
+def lg_step_bytes(B, L, gw=False):
     """One block of the long-block path (csrc/large.hip), per channel: the
-    canonical bytes (uniform_bytes) plus the four-step passes' own row
-    transfers, in rows of 8 B bytes: pass B re-reads pass A's FDL row and
-    rewrites it as the spectrum, writes pre_multiplied and the V scratch, and
-    pass C reads V back (5 rows)."""
-    return uniform_bytes(B, L) + 5 * 8 * B
+    canonical bytes (uniform_bytes; windowed_bytes when the batch runs on
+    far-row windows) plus the four-step passes' own row transfers, in rows of
+    8 B bytes: pass B re-reads pass A's FDL row and rewrites it as the
+    spectrum, writes pre_multiplied and the V scratch, and pass C reads V back
+    (5 rows)."""
+    return (windowed_bytes(B, L) if gw else uniform_bytes(B, L)) + 5 * 8 * B
 
 
 def run(conv, C, n_in, n_out, steps, warmup, ring, stream, update=None, batched=False):
@@ -360,10 +361,11 @@ def main():
         C, B, L = 64, 16384, 1000000
         conv = F.FFTConvolver.init(shard.synth_irs(range(C), L), B, L, channels=C)
         S = conv.seg_count
+        gw = conv.far_windows() > 0
         steps = max(8, a.steps2 // 16)
         t, ev = run(conv, C, B, B, steps, S + 2, 4, s, batched=True)
         samples = C * B * steps
-        per_sample = lg_step_bytes(B, L) / B
+        per_sample = lg_step_bytes(B, L, gw) / B
         out.append({"config": "lgu FFTConvolver on the long-block path", "channels": C, "block": B, "ir": L,
                     "segments": S, "steps": steps, "MSamples_s": round(samples / t / 1e6, 2),
                     "us_per_step": round(t / steps * 1e6, 3),
@@ -371,7 +373,8 @@ def main():
                     "frac_of_8TBs": round(samples * per_sample / t / 8e12, 4),
                     "bytes_per_sample": round(per_sample, 1),
                     "canonical_bytes_per_sample": round(uniform_bytes(B, L) / B, 1),
-                    "path": "lg_cols_fwd -> lg_rows (the FDL MAC) -> lg_cols_inv -> lg_call_end per call",
+                    "path": "lg_cols_fwd -> lg_rows (the FDL MAC) -> lg_cols_inv -> lg_call_end per call"
+                            + (" + gw_anchor_kernel (far-row windows, model: windowed_bytes)" if gw else ""),
                     "cfg": "lgu", "model_bytes_per_step": int(per_sample * C * B)})
         del conv
         if not a.no_cpu and not a.pmc_inner:

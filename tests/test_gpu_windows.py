@@ -1,5 +1,7 @@
 """Far-row windows of the generic step (1024 <= B <= 8192, >= 24 segments;
-csrc/kernels.hip gw_anchor_kernel).
+csrc/kernels.hip gw_anchor_kernel) and of the long-block path
+(2^14 <= B <= 2^22, csrc/large.hip lg_rows: the same windows, transposed bin
+order).
 
 FFTConvolver::process (src/fft_convolver.rs:215-295) with the FDL sum of a
 one-block call split as rows 1..P-1 (summed by the step) plus rows P..act-1
@@ -22,7 +24,7 @@ def _refs(oracle_mod, hs, B, L):
     return [oracle_mod.FFTConvolver.init(hs[c], B, L) for c in range(hs.shape[0])]
 
 
-@pytest.mark.parametrize("B,S", [(1024, 30), (2048, 26), (4096, 40), (8192, 25)])
+@pytest.mark.parametrize("B,S", [(1024, 30), (2048, 26), (4096, 40), (8192, 25), (16384, 25)])
 def test_windows_vs_oracle(amd, oracle_mod, B, S):
     """Entry, the ring wrapping, partial and multi-block calls, a batch update
     that shrinks act (ring index mod act), a channel update, a reset."""
@@ -59,11 +61,12 @@ def test_windows_vs_oracle(amd, oracle_mod, B, S):
             assert_close(got[c], refs[c].process(x[c]), what=f"after reset, block {j}")
 
 
-def test_windows_equal_full_sum(amd):
+@pytest.mark.parametrize("B", [1024, 16384])
+def test_windows_equal_full_sum(amd, B):
     """Steps served from windows give the same bits as steps that sum their
     far rows themselves (VARIANT_NOGW), through a partial call and re-entry."""
     rng = np.random.default_rng(710)
-    C, B, L = 13, 1024, 33 * 1024 + 7
+    C, L = 13, 33 * B + 7
     hs = np.stack([ir(rng, L) for _ in range(C)])
     ks = [B] * 40 + [300, B - 300] + [B] * 25 + [3 * B] + [B] * 10
     xs = [np.stack([white(rng, k) for _ in range(C)]) for k in ks]
@@ -90,11 +93,12 @@ def test_windows_class_independent(amd):
             assert np.array_equal(y[c], y[0]), (j, c)
 
 
-def test_windows_shards_and_clone(amd):
+@pytest.mark.parametrize("B", [1024, 16384])
+def test_windows_shards_and_clone(amd, B):
     """A 12-channel batch split 5 + 7 (every channel changes class and index)
     stays bit-identical; a clone taken mid-window continues bit-identically."""
     rng = np.random.default_rng(730)
-    C, B, L = 12, 1024, 28 * 1024
+    C, L = 12, 28 * B
     hs = np.stack([ir(rng, L) for _ in range(C)])
     one = amd.FFTConvolver.init(hs, B, L, channels=C)
     a = amd.FFTConvolver.init(hs[:5], B, L, channels=5)
@@ -108,12 +112,13 @@ def test_windows_shards_and_clone(amd):
         assert np.array_equal(one.process(x), twin.process(x)), j
 
 
-def test_windows_nan_block(amd, oracle_mod):
+@pytest.mark.parametrize("B", [1024, 16384])
+def test_windows_nan_block(amd, oracle_mod, B):
     """A non-finite block in one channel while its neighbours read windows:
     zero output, block kept in the input buffer, then recovery (the channel
     re-anchors) -- as the oracle."""
     rng = np.random.default_rng(740)
-    C, B, L = 9, 1024, 30 * 1024
+    C, L = 9, 30 * B
     hs = np.stack([ir(rng, L) for _ in range(C)])
     conv = amd.FFTConvolver.init(hs, B, L, channels=C)
     refs = _refs(oracle_mod, hs, B, L)
