@@ -45,6 +45,12 @@ namespace fftconv {
 namespace {
 
 constexpr int LG_NT = 256;
+// threads of a column-pass workgroup (passes A and C: one 4096-point tile
+// per workgroup, a few hundred workgroups per pass)
+#ifndef FFTCONV_LG_CNT
+#define FFTCONV_LG_CNT 256
+#endif
+constexpr int LG_CNT = FFTCONV_LG_CNT;
 constexpr int LG_E = 4096;  // complex points per column tile (passes A and C), at most
 // tiles per transform, at least (A/B builds: 8 or 16 tiles at B = 16384 --
 // 128..256-byte column runs -- measured 2-20% slower than 4 tiles of 512-byte
@@ -68,7 +74,7 @@ struct LgGeo {
     static constexpr size_t col_lds = 2 * (size_t)E * sizeof(float2);
     static constexpr size_t row_lds = 2 * 2 * (size_t)M2 * sizeof(float2);
     static_assert(LM >= 14 && LM <= 22, "long-block path: 2^14 <= B <= 2^22");
-    static_assert(TC >= 2 && TC <= M2 && EP >= 1 && E % LG_NT == 0 && E <= LG_E, "tile shape");
+    static_assert(TC >= 2 && TC <= M2 && EP >= 1 && E % LG_NT == 0 && E % LG_CNT == 0 && E <= LG_E, "tile shape");
 };
 
 // ---------------------------------------------------------------------------
@@ -82,13 +88,13 @@ __device__ __forceinline__ int bat(int b, int pos) {
     return IL ? pos * NB + b : (b << LF) + pos;
 }
 
-template <int LF, int NB, bool IL, bool INV, int S>
+template <int LF, int NB, bool IL, bool INV, int NT, int S>
 __device__ __forceinline__ void bstage(const float2 *src, float2 *dst, const float2 *__restrict__ tw, int tid) {
     constexpr int FL = 1 << LF, R4 = LF / 2;
     if constexpr (S < R4) {
         constexpr int Ns = 1 << (2 * S), Q = FL / 4;
         constexpr int step = FL / (2 * Ns);  // W_{2FL}^(m k step) = W_{4Ns}^(m k)
-        for (int e = tid; e < NB * Q; e += LG_NT) {
+        for (int e = tid; e < NB * Q; e += NT) {
             const int b = IL ? (e & (NB - 1)) : e / Q;
             const int j = IL ? e / NB : (e & (Q - 1));
             const int k = j & (Ns - 1);
@@ -111,7 +117,7 @@ __device__ __forceinline__ void bstage(const float2 *src, float2 *dst, const flo
         }
     } else {
         constexpr int H = FL / 2;  // the final radix-2 stage: Ns = FL / 2, k = j
-        for (int e = tid; e < NB * H; e += LG_NT) {
+        for (int e = tid; e < NB * H; e += NT) {
             const int b = IL ? (e & (NB - 1)) : e / H;
             const int j = IL ? e / NB : (e & (H - 1));
             const float2 v0 = src[bat<LF, NB, IL>(b, j)];
@@ -124,15 +130,15 @@ __device__ __forceinline__ void bstage(const float2 *src, float2 *dst, const flo
 
 // all stages from src (ping-pong with dst); returns the buffer holding the
 // naturally ordered result.  Every thread of the workgroup calls it.
-template <int LF, int NB, bool IL, bool INV, int S = 0>
+template <int LF, int NB, bool IL, bool INV, int NT = LG_NT, int S = 0>
 __device__ __forceinline__ float2 *bfft(float2 *src, float2 *dst, const float2 *__restrict__ tw, int tid) {
     constexpr int NS = LF / 2 + (LF & 1);
     if constexpr (S >= NS) {
         return src;
     } else {
-        bstage<LF, NB, IL, INV, S>(src, dst, tw, tid);
+        bstage<LF, NB, IL, INV, NT, S>(src, dst, tw, tid);
         __syncthreads();
-        return bfft<LF, NB, IL, INV, S + 1>(dst, src, tw, tid);
+        return bfft<LF, NB, IL, INV, NT, S + 1>(dst, src, tw, tid);
     }
 }
 
@@ -224,7 +230,7 @@ __device__ __forceinline__ bool lg_window(const LgPass &p, const Chunk &ch, int 
 // LG_IR: the H row itself; LG_RAW: scratch)
 // ---------------------------------------------------------------------------
 template <int LM, int MODE>
-__global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
+__global__ __launch_bounds__(LG_CNT) void lg_cols_fwd(LgPass p) {
     using G = LgGeo<LM>;
     constexpr int M = G::M, M1 = G::M1, M2 = G::M2, TC = G::TC;
     extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
             if (i >= ch.fill && i < ch.fill + ch.k) return inc[ch.processed + i - ch.fill];
             return inb ? ibc[i] : 0.f;
         };
-        for (int e = tid; e < G::E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_CNT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = n1 < M1 / 2 ? make_float2(x(2 * n), x(2 * n + 1)) : make_float2(0.f, 0.f);
@@ -262,7 +268,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
         const float *src = p.src + ch * p.src_stride;
         const long long base = (long long)s * M;  // (B = M samples per segment)
         auto x = [&](int i) -> float { return base + i < p.len_data ? src[base + i] : 0.f; };
-        for (int e = tid; e < G::E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_CNT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = n1 < M1 / 2 ? make_float2(x(2 * n), x(2 * n + 1)) : make_float2(0.f, 0.f);
@@ -270,15 +276,15 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_fwd(LgPass p) {
     } else {
         Y = p.Y + row * M;
         const float *in = p.in + (p.row0 + row) * p.in_stride;
-        for (int e = tid; e < G::E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_CNT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = make_float2(in[2 * n], in[2 * n + 1]);
         }
     }
     __syncthreads();
-    const float2 *R = bfft<G::L1, TC, true, false>(b0, b1, p.tb.twA, tid);
-    for (int e = tid; e < G::E; e += LG_NT) {
+    const float2 *R = bfft<G::L1, TC, true, false, LG_CNT>(b0, b1, p.tb.twA, tid);
+    for (int e = tid; e < G::E; e += LG_CNT) {
         const int t = e & (TC - 1), k1 = e / TC;
         const int n2 = c0 + t;
         DBG_CHECK(k1 < M1 && n2 < M2, 52, k1, n2, tile, (int)row);  // (site 52: pass A's Y position)
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
 //  LG_RAWINV: the rows, divided by N unless realfft flagged them (:42-46)
 // ---------------------------------------------------------------------------
 template <int LM, int MODE>
-__global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
+__global__ __launch_bounds__(LG_CNT) void lg_cols_inv(LgPass p) {
     using G = LgGeo<LM>;
     constexpr int M = G::M, M2 = G::M2, TC = G::TC, B = M;
     constexpr float invN = 1.0f / (float)(2 * M);
@@ -566,18 +572,18 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
     } else {
         V = p.Y + row * M;
     }
-    for (int e = tid; e < G::E; e += LG_NT) {
+    for (int e = tid; e < G::E; e += LG_CNT) {
         const int t = e & (TC - 1), k1 = e / TC;
         b0[e] = V[(size_t)k1 * M2 + c0 + t];
     }
     __syncthreads();
-    const float2 *R = bfft<G::L1, TC, true, true>(b0, b1, p.tb.twA, tid);
+    const float2 *R = bfft<G::L1, TC, true, true, LG_CNT>(b0, b1, p.tb.twA, tid);
 
     if constexpr (MODE == LG_RAWINV) {
         const float *in = p.in + (p.row0 + row) * p.in_stride;
         const float sc = (in[1] != 0.f || in[2 * M + 1] != 0.f) ? 1.0f : invN;  // (flagged rows stay unscaled)
         float *o = p.out + (p.row0 + row) * p.out_stride;
-        for (int e = tid; e < G::E; e += LG_NT) {
+        for (int e = tid; e < G::E; e += LG_CNT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const size_t n = (size_t)n1 * M2 + c0 + t;
             o[2 * n] = R[e].x * sc;
@@ -595,7 +601,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
         const int lo = ch.fill, hi = ch.fill + ch.k;
         const bool complete = hi == B;
         // the first half of the tile's rows (n1 < M1/2) holds samples j < B
-        for (int e = tid; e < G::E / 2; e += LG_NT) {
+        for (int e = tid; e < G::E / 2; e += LG_CNT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int j0 = 2 * (n1 * M2 + c0 + t);
 #pragma unroll
@@ -618,7 +624,7 @@ __global__ __launch_bounds__(LG_NT) void lg_cols_inv(LgPass p) {
         }
         if (complete && !err) {
             __syncthreads();  // every overlap read above is done (sample j and j + B share the column)
-            for (int e = G::E / 2 + tid; e < G::E; e += LG_NT) {
+            for (int e = G::E / 2 + tid; e < G::E; e += LG_CNT) {
                 const int t = e & (TC - 1), n1 = e / TC;
                 const int j = 2 * (n1 * M2 + c0 + t) - B;
                 ovc[j] = R[e].x * invN;  // :283-284
@@ -724,9 +730,9 @@ hipError_t lg_process_t(const ProcArgs &a, const LgTab &t, int chunks, int chann
         if (p.J.n <= 0) continue;
         if (hipError_t e = lds_attr(lg_rows<LM, LG_CONV>, G::row_lds); e != hipSuccess) return e;
         for (int it = 0; it < chunks; ++it) {
-            hipLaunchKernelGGL((lg_cols_fwd<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
+            hipLaunchKernelGGL((lg_cols_fwd<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
             hipLaunchKernelGGL((lg_rows<LM, LG_CONV>), dim3(channels * G::NPAIR), dim3(LG_NT), G::row_lds, s, p);
-            hipLaunchKernelGGL((lg_cols_inv<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
+            hipLaunchKernelGGL((lg_cols_inv<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
         }
         hipLaunchKernelGGL(lg_call_end, dim3(channels), dim3(256), 0, s, p.J);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
@@ -754,7 +760,7 @@ hipError_t lg_ir_t(const IrArgs &a, const LgTab &t, int channels, hipStream_t s)
         if (hipError_t e = lds_attr(lg_rows<LM, LG_IR>, G::row_lds); e != hipSuccess) return e;
         const long long rows = (long long)channels * nseg;
         if (rows * G::NPAIR > INT32_MAX) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((lg_cols_fwd<LM, LG_IR>), dim3((unsigned)(rows * G::NTILE)), dim3(LG_NT), G::col_lds, s, p);
+        hipLaunchKernelGGL((lg_cols_fwd<LM, LG_IR>), dim3((unsigned)(rows * G::NTILE)), dim3(LG_CNT), G::col_lds, s, p);
         hipLaunchKernelGGL((lg_rows<LM, LG_IR>), dim3((unsigned)(rows * G::NPAIR)), dim3(LG_NT), G::row_lds, s, p);
     }
     if (nseg < a.S) {  // segments past the response: zero (:210-212)
@@ -785,11 +791,11 @@ hipError_t lg_fft_t(bool inverse, const FftArgs &a, const LgTab &t, float2 *scra
         p.Y = scratch;
         p.row0 = r0;
         if (!inverse) {
-            hipLaunchKernelGGL((lg_cols_fwd<LM, LG_RAW>), dim3(n * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
+            hipLaunchKernelGGL((lg_cols_fwd<LM, LG_RAW>), dim3(n * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
             hipLaunchKernelGGL(kb, dim3(n * G::NPAIR), dim3(LG_NT), G::row_lds, s, p);
         } else {
             hipLaunchKernelGGL(kb, dim3(n * G::NPAIR), dim3(LG_NT), G::row_lds, s, p);
-            hipLaunchKernelGGL((lg_cols_inv<LM, LG_RAWINV>), dim3(n * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
+            hipLaunchKernelGGL((lg_cols_inv<LM, LG_RAWINV>), dim3(n * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
         }
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }

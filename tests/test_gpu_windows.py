@@ -135,10 +135,11 @@ def test_windows_nan_block(amd, oracle_mod, B):
             assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
 
 
-@pytest.mark.parametrize("head,L,T", [(32, 34000, 1024), (64, 70000, 2048)])
+@pytest.mark.parametrize("head,L,T", [(32, 34000, 1024), (64, 70000, 2048), (512, 450000, 16384)])
 def test_windows_twostage_tail(amd, oracle_mod, head, L, T):
-    """The two-stage tail (T = 1024 with 32 segments, T = 2048 with 33) runs
-    on windows: the output is the oracle's over 10 tail periods."""
+    """The two-stage tail (T = 1024 with 32 segments, T = 2048 with 33, and
+    the long-block path's T = 16384 with 26) runs on windows: the output is
+    the oracle's over 10 tail periods."""
     rng = np.random.default_rng(750 + head)
     h = ir(rng, L)
     conv = amd.TwoStageFFTConvolver.init(h, head, L)
