@@ -356,6 +356,10 @@ struct UniformCore {
         if (la_W) {
             const LaDims d = la_dims(log2b, (int)S);
             if (int r = laW.alloc(C * 2 * (size_t)d.pt * B)) return r;
+            // (tests: FFTCONV_LA_POISON=1 fills the windows with NaN at init, so a
+            // window row read before any anchor wrote it shows in the output)
+            if (const char *e = getenv("FFTCONV_LA_POISON"); e && atoi(e) > 0)
+                HIP_TRY(hipMemset(laW.p, 0xff, laW.bytes()));
             if (const char *e = getenv("FFTCONV_LA_PROBE"); e && atoi(e) > 0) {
                 if (int r = la_probe.alloc(1)) return r;
                 HIP_TRY(hipMemset(la_probe.p, 0, sizeof(int)));

@@ -31,7 +31,10 @@ from fftconv_amd import shard  # noqa: E402
 def run(conv, d_in, in_stride, in_step, C, B, NB):
     dev = torch.device("cuda:0")
     yd = torch.empty(NB, C, B, device=dev)
-    s = torch.cuda.current_stream(dev)
+    # an explicit stream, ordered after the default stream's work: stream 0 would
+    # select the handle's own stream (fftconv.h), which the default stream does not wait for
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
     conv.process_device_steps(d_in.data_ptr(), in_stride, in_step, yd.data_ptr(), B, C * B, B, NB, s.cuda_stream)
     s.synchronize()
     return yd.cpu().numpy()
@@ -42,6 +45,8 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     t0 = time.time()
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if os.environ.get("FFTCONV_TEST_VARIANT"):  # (diagnostics: scripts/cfg4_diag.py)
+        F.set_kernel_variant(int(os.environ["FFTCONV_TEST_VARIANT"]))
     mine = shard.channel_range(rank, world, C)
     dev = torch.device("cuda:0")
     irs = shard.synth_irs(mine, L)

@@ -29,7 +29,10 @@ def main():
              else torch.zeros(NB, B, device=dev))
         shard.broadcast_dry(dist, t, src=0)
         yd = torch.empty(NB, C, B, device=dev)
-        s = torch.cuda.current_stream(dev)
+        # an explicit stream, ordered after the default stream's work: stream 0 would
+        # select the handle's own stream (fftconv.h), which the default stream does not wait for
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
         for b in range(NB):
             conv.process_device(t[b].data_ptr(), 0, yd[b].data_ptr(), B, B, s.cuda_stream)
         s.synchronize()

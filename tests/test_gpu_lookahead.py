@@ -175,6 +175,57 @@ def test_lookahead_device_steps(amd, oracle_mod):
                      what=f"channel {c}")
 
 
+@pytest.mark.parametrize("C,B", [(8, 256), (64, 256), (64, 512)])
+def test_lookahead_windows_never_read_unwritten(amd, monkeypatch, C, B):
+    """FFTCONV_LA_POISON fills the window buffer with NaN at init: no step may
+    read a window row before an anchor (or the init / reset rebuild) wrote it,
+    so the output stays finite and bit-identical to an unpoisoned handle --
+    through a reset, over more than a level-3 period."""
+    import torch
+
+    rng = np.random.default_rng(370 + C + B)
+    L, K = 188 * B, 200
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    xd = torch.from_numpy(np.stack([white(rng, C * B).reshape(C, B) for _ in range(K)])).to("cuda:0")
+    outs = []
+    for poison in ("1", "0"):
+        monkeypatch.setenv("FFTCONV_LA_POISON", poison)
+        conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+        monkeypatch.delenv("FFTCONV_LA_POISON")
+        assert conv.lookahead_parts() > 0
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        for _ in range(2):  # (the second pass after a reset)
+            yd = torch.empty_like(xd)
+            conv.process_device_steps(xd.data_ptr(), B, C * B, yd.data_ptr(), B, C * B, B, K, s.cuda_stream)
+            s.synchronize()
+            outs.append(yd.cpu().numpy())
+            conv.reset()
+    assert np.isfinite(outs[0]).all() and np.isfinite(outs[1]).all()
+    for y in outs[1:]:
+        assert np.array_equal(y, outs[0])
+
+
+def test_device_stream_zero_is_the_handle_stream(amd):
+    """stream 0 selects the handle's own stream (fftconv.h), not the default
+    HIP stream: after synchronize() the output is complete and equals the
+    same calls on an explicit stream."""
+    import torch
+
+    rng = np.random.default_rng(380)
+    C, B, L, K = 16, 256, 48 * 256, 64
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    xd = torch.from_numpy(np.stack([white(rng, C * B).reshape(C, B) for _ in range(K)])).to("cuda:0")
+    a, b = amd.FFTConvolver.init(hs, B, L, channels=C), amd.FFTConvolver.init(hs, B, L, channels=C)
+    ya, yb = torch.empty_like(xd), torch.empty_like(xd)
+    a.process_device_steps(xd.data_ptr(), B, C * B, ya.data_ptr(), B, C * B, B, K, 0)
+    a.synchronize()
+    s = torch.cuda.Stream()
+    b.process_device_steps(xd.data_ptr(), B, C * B, yb.data_ptr(), B, C * B, B, K, s.cuda_stream)
+    s.synchronize()
+    assert np.array_equal(ya.cpu().numpy(), yb.cpu().numpy())
+
+
 @pytest.mark.parametrize("B,L", [(256, 40 * 256 + 5), (512, 44 * 512)])
 def test_lookahead_crossfade_vs_oracle(amd, oracle_mod, B, L):
     """CrossfadeConvolver<FFTConvolver> (src/crossfade_convolver.rs:45-105)
