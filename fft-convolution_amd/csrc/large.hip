@@ -45,12 +45,13 @@ namespace fftconv {
 namespace {
 
 constexpr int LG_NT = 256;
-// threads of a column-pass workgroup (passes A and C: one 4096-point tile
-// per workgroup, a few hundred workgroups per pass)
-#ifndef FFTCONV_LG_CNT
-#define FFTCONV_LG_CNT 256
-#endif
-constexpr int LG_CNT = FFTCONV_LG_CNT;
+// threads of a column-pass workgroup of a convolution pass (A and C: one
+// 4096-point tile per workgroup).  With fewer tiles than two per CU the pass
+// runs one wave per SIMD at 256 threads; LG_CNT_WIDE threads per tile then
+// hide its latency (lgu, 256 tiles: 113.7 -> 101.7 us per step, A/B
+// r5aa_ab_lg_cnt.log); larger grids keep 256.
+constexpr int LG_CNT_WIDE = 1024;
+constexpr int LG_WIDE_MAX_TILES = 512;
 constexpr int LG_E = 4096;  // complex points per column tile (passes A and C), at most
 // tiles per transform, at least (A/B builds: 8 or 16 tiles at B = 16384 --
 // 128..256-byte column runs -- measured 2-20% slower than 4 tiles of 512-byte
@@ -74,7 +75,7 @@ struct LgGeo {
     static constexpr size_t col_lds = 2 * (size_t)E * sizeof(float2);
     static constexpr size_t row_lds = 2 * 2 * (size_t)M2 * sizeof(float2);
     static_assert(LM >= 14 && LM <= 22, "long-block path: 2^14 <= B <= 2^22");
-    static_assert(TC >= 2 && TC <= M2 && EP >= 1 && E % LG_NT == 0 && E % LG_CNT == 0 && E <= LG_E, "tile shape");
+    static_assert(TC >= 2 && TC <= M2 && EP >= 1 && E % LG_NT == 0 && E % LG_CNT_WIDE == 0 && E <= LG_E, "tile shape");
 };
 
 // ---------------------------------------------------------------------------
@@ -229,8 +230,8 @@ __device__ __forceinline__ bool lg_window(const LgPass &p, const Chunk &ch, int 
 // (LG_CONV: Y is the FDL row `current`, overwritten by pass B's spectrum;
 // LG_IR: the H row itself; LG_RAW: scratch)
 // ---------------------------------------------------------------------------
-template <int LM, int MODE>
-__global__ __launch_bounds__(LG_CNT) void lg_cols_fwd(LgPass p) {
+template <int LM, int MODE, int NT = LG_NT>
+__global__ __launch_bounds__(NT) void lg_cols_fwd(LgPass p) {
     using G = LgGeo<LM>;
     constexpr int M = G::M, M1 = G::M1, M2 = G::M2, TC = G::TC;
     extern __shared__ __attribute__((aligned(16))) unsigned char lg_smem[];
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(LG_CNT) void lg_cols_fwd(LgPass p) {
             if (i >= ch.fill && i < ch.fill + ch.k) return inc[ch.processed + i - ch.fill];
             return inb ? ibc[i] : 0.f;
         };
-        for (int e = tid; e < G::E; e += LG_CNT) {
+        for (int e = tid; e < G::E; e += NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = n1 < M1 / 2 ? make_float2(x(2 * n), x(2 * n + 1)) : make_float2(0.f, 0.f);
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(LG_CNT) void lg_cols_fwd(LgPass p) {
         const float *src = p.src + ch * p.src_stride;
         const long long base = (long long)s * M;  // (B = M samples per segment)
         auto x = [&](int i) -> float { return base + i < p.len_data ? src[base + i] : 0.f; };
-        for (int e = tid; e < G::E; e += LG_CNT) {
+        for (int e = tid; e < G::E; e += NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = n1 < M1 / 2 ? make_float2(x(2 * n), x(2 * n + 1)) : make_float2(0.f, 0.f);
@@ -276,15 +277,15 @@ __global__ __launch_bounds__(LG_CNT) void lg_cols_fwd(LgPass p) {
     } else {
         Y = p.Y + row * M;
         const float *in = p.in + (p.row0 + row) * p.in_stride;
-        for (int e = tid; e < G::E; e += LG_CNT) {
+        for (int e = tid; e < G::E; e += NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int n = n1 * M2 + c0 + t;
             b0[e] = make_float2(in[2 * n], in[2 * n + 1]);
         }
     }
     __syncthreads();
-    const float2 *R = bfft<G::L1, TC, true, false, LG_CNT>(b0, b1, p.tb.twA, tid);
-    for (int e = tid; e < G::E; e += LG_CNT) {
+    const float2 *R = bfft<G::L1, TC, true, false, NT>(b0, b1, p.tb.twA, tid);
+    for (int e = tid; e < G::E; e += NT) {
         const int t = e & (TC - 1), k1 = e / TC;
         const int n2 = c0 + t;
         DBG_CHECK(k1 < M1 && n2 < M2, 52, k1, n2, tile, (int)row);  // (site 52: pass A's Y position)
@@ -552,8 +553,8 @@ __global__ __launch_bounds__(LG_NT) void lg_rows(LgPass p) {
 //           block state (:277-292) and the call's progress
 //  LG_RAWINV: the rows, divided by N unless realfft flagged them (:42-46)
 // ---------------------------------------------------------------------------
-template <int LM, int MODE>
-__global__ __launch_bounds__(LG_CNT) void lg_cols_inv(LgPass p) {
+template <int LM, int MODE, int NT = LG_NT>
+__global__ __launch_bounds__(NT) void lg_cols_inv(LgPass p) {
     using G = LgGeo<LM>;
     constexpr int M = G::M, M2 = G::M2, TC = G::TC, B = M;
     constexpr float invN = 1.0f / (float)(2 * M);
@@ -572,18 +573,18 @@ __global__ __launch_bounds__(LG_CNT) void lg_cols_inv(LgPass p) {
     } else {
         V = p.Y + row * M;
     }
-    for (int e = tid; e < G::E; e += LG_CNT) {
+    for (int e = tid; e < G::E; e += NT) {
         const int t = e & (TC - 1), k1 = e / TC;
         b0[e] = V[(size_t)k1 * M2 + c0 + t];
     }
     __syncthreads();
-    const float2 *R = bfft<G::L1, TC, true, true, LG_CNT>(b0, b1, p.tb.twA, tid);
+    const float2 *R = bfft<G::L1, TC, true, true, NT>(b0, b1, p.tb.twA, tid);
 
     if constexpr (MODE == LG_RAWINV) {
         const float *in = p.in + (p.row0 + row) * p.in_stride;
         const float sc = (in[1] != 0.f || in[2 * M + 1] != 0.f) ? 1.0f : invN;  // (flagged rows stay unscaled)
         float *o = p.out + (p.row0 + row) * p.out_stride;
-        for (int e = tid; e < G::E; e += LG_CNT) {
+        for (int e = tid; e < G::E; e += NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const size_t n = (size_t)n1 * M2 + c0 + t;
             o[2 * n] = R[e].x * sc;
@@ -601,7 +602,7 @@ __global__ __launch_bounds__(LG_CNT) void lg_cols_inv(LgPass p) {
         const int lo = ch.fill, hi = ch.fill + ch.k;
         const bool complete = hi == B;
         // the first half of the tile's rows (n1 < M1/2) holds samples j < B
-        for (int e = tid; e < G::E / 2; e += LG_CNT) {
+        for (int e = tid; e < G::E / 2; e += NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int j0 = 2 * (n1 * M2 + c0 + t);
 #pragma unroll
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(LG_CNT) void lg_cols_inv(LgPass p) {
         }
         if (complete && !err) {
             __syncthreads();  // every overlap read above is done (sample j and j + B share the column)
-            for (int e = G::E / 2 + tid; e < G::E; e += LG_CNT) {
+            for (int e = G::E / 2 + tid; e < G::E; e += NT) {
                 const int t = e & (TC - 1), n1 = e / TC;
                 const int j = 2 * (n1 * M2 + c0 + t) - B;
                 ovc[j] = R[e].x * invN;  // :283-284
@@ -729,10 +730,19 @@ hipError_t lg_process_t(const ProcArgs &a, const LgTab &t, int chunks, int chann
         if (!p.J.lg_prog || !p.J.lg_v) return hipErrorInvalidValue;
         if (p.J.n <= 0) continue;
         if (hipError_t e = lds_attr(lg_rows<LM, LG_CONV>, G::row_lds); e != hipSuccess) return e;
+        const bool wide = (long long)channels * G::NTILE <= LG_WIDE_MAX_TILES;
         for (int it = 0; it < chunks; ++it) {
-            hipLaunchKernelGGL((lg_cols_fwd<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
+            if (wide)
+                hipLaunchKernelGGL((lg_cols_fwd<LM, LG_CONV, LG_CNT_WIDE>), dim3(channels * G::NTILE), dim3(LG_CNT_WIDE),
+                                   G::col_lds, s, p);
+            else
+                hipLaunchKernelGGL((lg_cols_fwd<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
             hipLaunchKernelGGL((lg_rows<LM, LG_CONV>), dim3(channels * G::NPAIR), dim3(LG_NT), G::row_lds, s, p);
-            hipLaunchKernelGGL((lg_cols_inv<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
+            if (wide)
+                hipLaunchKernelGGL((lg_cols_inv<LM, LG_CONV, LG_CNT_WIDE>), dim3(channels * G::NTILE), dim3(LG_CNT_WIDE),
+                                   G::col_lds, s, p);
+            else
+                hipLaunchKernelGGL((lg_cols_inv<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
         }
         hipLaunchKernelGGL(lg_call_end, dim3(channels), dim3(256), 0, s, p.J);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
@@ -760,7 +770,7 @@ hipError_t lg_ir_t(const IrArgs &a, const LgTab &t, int channels, hipStream_t s)
         if (hipError_t e = lds_attr(lg_rows<LM, LG_IR>, G::row_lds); e != hipSuccess) return e;
         const long long rows = (long long)channels * nseg;
         if (rows * G::NPAIR > INT32_MAX) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((lg_cols_fwd<LM, LG_IR>), dim3((unsigned)(rows * G::NTILE)), dim3(LG_CNT), G::col_lds, s, p);
+        hipLaunchKernelGGL((lg_cols_fwd<LM, LG_IR>), dim3((unsigned)(rows * G::NTILE)), dim3(LG_NT), G::col_lds, s, p);
         hipLaunchKernelGGL((lg_rows<LM, LG_IR>), dim3((unsigned)(rows * G::NPAIR)), dim3(LG_NT), G::row_lds, s, p);
     }
     if (nseg < a.S) {  // segments past the response: zero (:210-212)
@@ -791,11 +801,11 @@ hipError_t lg_fft_t(bool inverse, const FftArgs &a, const LgTab &t, float2 *scra
         p.Y = scratch;
         p.row0 = r0;
         if (!inverse) {
-            hipLaunchKernelGGL((lg_cols_fwd<LM, LG_RAW>), dim3(n * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
+            hipLaunchKernelGGL((lg_cols_fwd<LM, LG_RAW>), dim3(n * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
             hipLaunchKernelGGL(kb, dim3(n * G::NPAIR), dim3(LG_NT), G::row_lds, s, p);
         } else {
             hipLaunchKernelGGL(kb, dim3(n * G::NPAIR), dim3(LG_NT), G::row_lds, s, p);
-            hipLaunchKernelGGL((lg_cols_inv<LM, LG_RAWINV>), dim3(n * G::NTILE), dim3(LG_CNT), G::col_lds, s, p);
+            hipLaunchKernelGGL((lg_cols_inv<LM, LG_RAWINV>), dim3(n * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
         }
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
