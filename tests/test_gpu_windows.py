@@ -175,3 +175,31 @@ def test_windows_device_steps(amd, oracle_mod):
         ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
         assert_close(y[c], np.concatenate([ref.process(x[c, k * B:(k + 1) * B]) for k in range(K)]),
                      what=f"channel {c}")
+
+
+@pytest.mark.parametrize("B,C", [(32768, 3), (131072, 2)])
+def test_windows_long_blocks(amd, oracle_mod, B, C):
+    """Far-row windows past B = 16384 (gw_anchor_kernel<15..17>, lg_rows):
+    the oracle over S + 10 one-block calls with a partial call in the middle,
+    and bit-identical to summing every far row (VARIANT_NOGW)."""
+    rng = np.random.default_rng(790 + B)
+    S = 25
+    L = S * B - 3
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    ks = [B] * (S + 2) + [B // 5, B - B // 5] + [B] * 9
+    xs = [np.stack([white(rng, k) for _ in range(C)]) for k in ks]
+    outs = {}
+    for v in (-1, NOGW):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+            assert conv.far_windows() == 8
+            outs[v] = [conv.process(x) for x in xs]
+        finally:
+            amd.set_kernel_variant(-1)
+    for a, b in zip(outs[-1], outs[NOGW]):
+        assert np.array_equal(a, b)
+    refs = _refs(oracle_mod, hs, B, L)
+    for j, (x, got) in enumerate(zip(xs, outs[-1])):
+        for c in range(C):
+            assert_close(got[c], refs[c].process(x[c]), what=f"B={B} call {j} ch {c}")
