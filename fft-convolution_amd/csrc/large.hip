@@ -212,6 +212,10 @@ struct LgPass {
     // LG_CONV far-row windows (ProcArgs::gw_p / gw / gw_t)
     const float2 *gw;
     int gw_p, gw_t;
+    // LG_CONV: a one-chunk call with no two-stage epilogue -- pass C ends it
+    // (what lg_call_end does otherwise: zero output for a channel without
+    // active segments or with a failed C2R, progress words reset)
+    int end_fused;
 };
 
 // the far-row split of a channel's pre_multiplied (0 = one sum) and whether
@@ -568,7 +572,17 @@ __global__ __launch_bounds__(NT) void lg_cols_inv(LgPass p) {
     const float2 *V;
     if constexpr (MODE == LG_CONV) {
         ch = lg_chunk<LM>(p.J, row);
-        if (!ch.go) return;
+        if (!ch.go) {
+            if (p.end_fused) {  // (one chunk: !go = no active segment) output.fill(0) (:216-219), this tile's samples
+                float *outc = p.J.out + row * p.J.out_stride;
+                for (int e = tid; e < G::E / 2; e += NT) {
+                    const int j0 = 2 * ((e / TC) * M2 + c0 + (e & (TC - 1)));
+                    if (j0 < p.J.n) outc[j0] = 0.f;
+                    if (j0 + 1 < p.J.n) outc[j0 + 1] = 0.f;
+                }
+            }
+            return;
+        }
         V = p.J.lg_v + row * M;
     } else {
         V = p.Y + row * M;
@@ -610,8 +624,12 @@ __global__ __launch_bounds__(NT) void lg_cols_inv(LgPass p) {
                 const int j = j0 + q;
                 if (err) {
                     // output.fill(0); return (:264-267): the chunk stays in
-                    // the input buffer (lg_call_end zero-fills the output)
-                    if (j >= lo && j < hi) ibc[j] = inc[ch.processed + j - lo];
+                    // the input buffer (lg_call_end zero-fills the output,
+                    // or this pass when it ends the call)
+                    if (j >= lo && j < hi) {
+                        ibc[j] = inc[ch.processed + j - lo];
+                        if (p.end_fused) outc[ch.processed + j - lo] = 0.f;
+                    }
                     continue;
                 }
                 DBG_CHECK(j < B && (j < lo || j >= hi || ch.processed + j - lo < J.n), 56, j, lo, hi, ch.processed);
@@ -659,6 +677,11 @@ __global__ __launch_bounds__(NT) void lg_cols_inv(LgPass p) {
                         fill += ch.k;
                     }
                     pg[0] = ch.processed + ch.k;
+                }
+                if (p.end_fused) {  // the call ends here: progress words reset (every tile has read them)
+                    pg[0] = 0;
+                    pg[1] = 0;
+                    pg[2] = 0;
                 }
                 J.state[row] = make_int4(cur, ch.act, fill, flags);
             }
@@ -731,6 +754,10 @@ hipError_t lg_process_t(const ProcArgs &a, const LgTab &t, int chunks, int chann
         if (p.J.n <= 0) continue;
         if (hipError_t e = lds_attr(lg_rows<LM, LG_CONV>, G::row_lds); e != hipSuccess) return e;
         const bool wide = (long long)channels * G::NTILE <= LG_WIDE_MAX_TILES;
+#ifndef FFTCONV_LG_END_FUSED
+#define FFTCONV_LG_END_FUSED 1
+#endif
+        p.end_fused = FFTCONV_LG_END_FUSED && chunks == 1 && !p.J.add0 && !p.J.tin;
         for (int it = 0; it < chunks; ++it) {
             if (wide)
                 hipLaunchKernelGGL((lg_cols_fwd<LM, LG_CONV, LG_CNT_WIDE>), dim3(channels * G::NTILE), dim3(LG_CNT_WIDE),
@@ -744,7 +771,7 @@ hipError_t lg_process_t(const ProcArgs &a, const LgTab &t, int chunks, int chann
             else
                 hipLaunchKernelGGL((lg_cols_inv<LM, LG_CONV>), dim3(channels * G::NTILE), dim3(LG_NT), G::col_lds, s, p);
         }
-        hipLaunchKernelGGL(lg_call_end, dim3(channels), dim3(256), 0, s, p.J);
+        if (!p.end_fused) hipLaunchKernelGGL(lg_call_end, dim3(channels), dim3(256), 0, s, p.J);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -178,6 +178,39 @@ def test_uniform_large_nonfinite(amd, oracle_mod):
         assert conv.channel_state() == (ref.current, ref.active_seg_count, ref.fill)
 
 
+def test_uniform_large_empty_response_and_nan_batch(amd, oracle_mod):
+    """One-block calls (pass C ends the call, no lg_call_end): a channel whose
+    response is updated to nothing has no active segment and outputs zeros
+    (:216-219) while its neighbours convolve, a NaN block in one channel
+    zero-fills that call (:264-267), then a full response again -- every
+    channel as the oracle, state words included."""
+    rng = np.random.default_rng(78)
+    C, B, L = 3, 16384, 3 * 16384
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    conv = amd.FFTConvolver.init(hs, B, L, channels=C)
+    refs = [oracle_mod.FFTConvolver.init(hs[c], B, L) for c in range(C)]
+    for i in range(10):
+        if i == 2:
+            conv.update_channel(1, np.zeros(0, np.float32))
+            refs[1].update(np.zeros(0, np.float32))
+        if i == 7:
+            h1 = ir(rng, L)
+            conv.update_channel(1, h1)
+            refs[1].update(h1)
+        x = np.stack([white(rng, B) for _ in range(C)])
+        if i == 4:
+            x[2, 50] = np.nan
+        got = conv.process(x)
+        for c in range(C):
+            r = refs[c].process(x[c])
+            assert np.array_equal(np.isnan(got[c]), np.isnan(r)), (i, c)
+            m = ~np.isnan(r)
+            assert_close(got[c][m], r[m], what=f"call {i} ch {c}")
+            assert conv.channel_state(c) == (refs[c].current, refs[c].active_seg_count, refs[c].fill)
+        if 2 <= i < 7:
+            assert not got[1].any()
+
+
 @pytest.mark.parametrize("head,L", [(512, 200000), (1024, 1000000)])
 def test_twostage_long_tail_vs_oracle(amd, oracle_mod, head, L):
     """TwoStageFFTConvolver (:323-512) whose tail block exceeds 8192:
