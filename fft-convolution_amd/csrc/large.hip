@@ -615,8 +615,21 @@ __global__ __launch_bounds__(NT) void lg_cols_inv(LgPass p) {
         float *ibc = J.inbuf + row * B;
         const int lo = ch.fill, hi = ch.fill + ch.k;
         const bool complete = hi == B;
-        // the first half of the tile's rows (n1 < M1/2) holds samples j < B
-        for (int e = tid; e < G::E / 2; e += NT) {
+        // the first half of the tile's rows (n1 < M1/2) holds samples j < B;
+        // a whole block into an 8-byte aligned output goes out as sample pairs
+        const bool pairs = !err && lo == 0 && complete &&
+                           (reinterpret_cast<uintptr_t>(outc + ch.processed) & 7) == 0;
+        if (pairs) {
+            for (int e = tid; e < G::E / 2; e += NT) {
+                const int j0 = 2 * ((e / TC) * M2 + c0 + (e & (TC - 1)));
+                DBG_CHECK(j0 + 1 < B && ch.processed + j0 + 1 < J.n, 56, j0, lo, hi, ch.processed);
+                const float2 o = *reinterpret_cast<const float2 *>(ovc + j0);
+                *reinterpret_cast<float2 *>(outc + ch.processed + j0) =
+                    make_float2(R[e].x * invN + o.x, R[e].y * invN + o.y);  // :270-274
+                if (ch.flags & FLAG_INBUF) *reinterpret_cast<float2 *>(ibc + j0) = make_float2(0.f, 0.f);  // :280
+            }
+        }
+        for (int e = tid; e < (pairs ? 0 : G::E / 2); e += NT) {
             const int t = e & (TC - 1), n1 = e / TC;
             const int j0 = 2 * (n1 * M2 + c0 + t);
 #pragma unroll
@@ -646,8 +659,7 @@ __global__ __launch_bounds__(NT) void lg_cols_inv(LgPass p) {
             for (int e = G::E / 2 + tid; e < G::E; e += NT) {
                 const int t = e & (TC - 1), n1 = e / TC;
                 const int j = 2 * (n1 * M2 + c0 + t) - B;
-                ovc[j] = R[e].x * invN;  // :283-284
-                ovc[j + 1] = R[e].y * invN;
+                *reinterpret_cast<float2 *>(ovc + j) = make_float2(R[e].x * invN, R[e].y * invN);  // :283-284
             }
         }
         // the channel's last workgroup of this pass writes the block state
