@@ -994,6 +994,66 @@ __device__ __forceinline__ bool process_job(const ProcArgs &a, const ProcJob &J,
 // far rows itself.  A workgroup: one channel, 256 slots (512 bins).  Channels
 // whose ring is off the block path (a buffered partial block, a failed C2R)
 // or too short get no window: FLAG_GW cleared.
+// long blocks (B > 2^kMaxLog2Fused): windows K0 .. K0+KH-1 of one slot, the
+// far rows walked P at a time, software-pipelined (the next P rows' loads
+// issued before this batch's MACs); each window sums its rows in the same
+// order and arithmetic as the full walk below
+#ifndef FFTCONV_GW_SPLIT
+#define FFTCONV_GW_SPLIT 1  // threads per slot (2: window halves per thread, 41.9 vs 30.4 us at lgu, rejected)
+#endif
+template <int LOG2B, int K0, int KH>
+__device__ __forceinline__ void gw_walk_long(Acc2 (&w)[KH], const float4 *H4, const float4 *X4, int cur, int act) {
+    constexpr int F = (1 << LOG2B) / 2, P = kGwP;
+    float4 xr[P];  // X at ring offset o (from cur') in xr[o % P]
+#pragma unroll
+    for (int o = 1; o < P; ++o) xr[o] = ntld4(X4 + (size_t)((cur + o) % act) * F);
+    xr[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int i0 = P;
+    float4 h[P], xn[P];
+    if (i0 + P <= act) {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
+            xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
+        }
+    }
+    for (; i0 + P <= act; i0 += P) {
+        float4 h2[P], x2[P];
+        const bool more = i0 + 2 * P <= act;
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                h2[j] = ntld4(H4 + (size_t)(i0 + P + j) * F);
+                x2[j] = ntld4(X4 + (size_t)((cur + i0 + P + j) % act) * F);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int kk = 0; kk < KH; ++kk) {
+                const int k = K0 + kk;
+                w[kk].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
+            }
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            xr[j] = xn[j];
+            if (more) {
+                h[j] = h2[j];
+                xn[j] = x2[j];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        if (i0 + j < act) {
+            const float4 hv = ntld4(H4 + (size_t)(i0 + j) * F);
+            xr[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
+#pragma unroll
+            for (int kk = 0; kk < KH; ++kk) w[kk].mac(hv, xr[(j - (K0 + kk) + P) % P]);
+        }
+    }
+}
+
 template <int LOG2B>
 __global__ __launch_bounds__(256) void gw_anchor_kernel(ProcArgs a) {
     constexpr int B = 1 << LOG2B, F = B / 2, P = kGwP;
@@ -1007,8 +1067,35 @@ __global__ __launch_bounds__(256) void gw_anchor_kernel(ProcArgs a) {
         if (blockIdx.x == 0 && threadIdx.x == 0) J.state[c].w = st.w & ~FLAG_GW;
         return;
     }
-    const int f = (int)blockIdx.x * 256 + (int)threadIdx.x;  // float4 slot
     const size_t rows = (size_t)J.S * B;
+    if constexpr (LOG2B > kMaxLog2Fused) {
+        // long blocks: FFTCONV_GW_SPLIT threads per slot, each summing P / SPLIT
+        // of the windows (SPLIT 2 doubles the waves, one per SIMD at 1, but
+        // measured slower: anchor 41.9 vs 30.4 us at lgu, r5ar)
+        constexpr int SPLIT = FFTCONV_GW_SPLIT, KH = P / SPLIT, SL = 256 / SPLIT;
+        static_assert(P % SPLIT == 0 && SL % 64 == 0, "window split");
+        const int part = (int)threadIdx.x / SL;  // (wave-uniform)
+        const int f = (int)blockIdx.x * SL + (int)threadIdx.x % SL;
+        const float4 *H4 = reinterpret_cast<const float4 *>(J.H + (size_t)c * rows) + f;
+        const float4 *X4 = reinterpret_cast<const float4 *>(J.X + (size_t)c * rows) + f;
+        Acc2 w[KH];
+#pragma unroll
+        for (int k = 0; k < KH; ++k) w[k].zero();
+        if constexpr (SPLIT == 1) {
+            gw_walk_long<LOG2B, 0, KH>(w, H4, X4, cur, act);
+        } else if constexpr (SPLIT == 2) {
+            if (part == 0) gw_walk_long<LOG2B, 0, KH>(w, H4, X4, cur, act);
+            else gw_walk_long<LOG2B, KH, KH>(w, H4, X4, cur, act);
+        } else {
+            static_assert(SPLIT <= 2, "window split");
+        }
+        float4 *W4 = reinterpret_cast<float4 *>(a.gw + (size_t)c * P * B) + f;
+#pragma unroll
+        for (int k = 0; k < KH; ++k) ntst4(W4 + (size_t)(part * KH + k) * F, w[k].get(f));
+        if (blockIdx.x == 0 && threadIdx.x == 0) J.state[c].w = st.w | FLAG_GW;
+        return;
+    }
+    const int f = (int)blockIdx.x * 256 + (int)threadIdx.x;  // float4 slot
     const float4 *H4 = reinterpret_cast<const float4 *>(J.H + (size_t)c * rows) + f;
     const float4 *X4 = reinterpret_cast<const float4 *>(J.X + (size_t)c * rows) + f;
     Acc2 w[P];
@@ -1020,59 +1107,23 @@ __global__ __launch_bounds__(256) void gw_anchor_kernel(ProcArgs a) {
         DBG_CHECK((cur + o) % act < J.S, 41, cur, o, act, J.S);
         xr[o] = ntld4(X4 + (size_t)((cur + o) % act) * F);
     }
-    // P rows in flight; on the long-block path (one wave per SIMD: latency is
-    // not hidden by other waves) software-pipelined: the next P rows' loads
-    // are issued before this batch's MACs.  (The two-stage tail's anchor at
-    // B <= 8192 runs beside the head on few CUs: the plain loop's lower
-    // register count measured faster there.)
+    // P rows in flight (B <= 8192: the two-stage tail's anchor beside the
+    // head on few CUs -- the plain loop's lower register count measured
+    // faster there than the pipelined walk of gw_walk_long)
     int i0 = P;
-    if constexpr (LOG2B > kMaxLog2Fused) {
+    for (; i0 + P <= act; i0 += P) {
         float4 h[P], xn[P];
-        if (i0 + P <= act) {
 #pragma unroll
-            for (int j = 0; j < P; ++j) {
-                h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
-                xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
-            }
+        for (int j = 0; j < P; ++j) {
+            h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
+            xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
         }
-        for (; i0 + P <= act; i0 += P) {
-            float4 h2[P], x2[P];
-            const bool more = i0 + 2 * P <= act;
-            if (more) {
 #pragma unroll
-                for (int j = 0; j < P; ++j) {
-                    h2[j] = ntld4(H4 + (size_t)(i0 + P + j) * F);
-                    x2[j] = ntld4(X4 + (size_t)((cur + i0 + P + j) % act) * F);
-                }
-            }
+        for (int j = 0; j < P; ++j)
 #pragma unroll
-            for (int j = 0; j < P; ++j)
+            for (int k = 0; k < P; ++k) w[k].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
 #pragma unroll
-                for (int k = 0; k < P; ++k) w[k].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                xr[j] = xn[j];
-                if (more) {
-                    h[j] = h2[j];
-                    xn[j] = x2[j];
-                }
-            }
-        }
-    } else {
-        for (; i0 + P <= act; i0 += P) {
-            float4 h[P], xn[P];
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                h[j] = ntld4(H4 + (size_t)(i0 + j) * F);
-                xn[j] = ntld4(X4 + (size_t)((cur + i0 + j) % act) * F);
-            }
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-#pragma unroll
-                for (int k = 0; k < P; ++k) w[k].mac(h[j], j >= k ? xn[j - k] : xr[j - k + P]);
-#pragma unroll
-            for (int j = 0; j < P; ++j) xr[j] = xn[j];
-        }
+        for (int j = 0; j < P; ++j) xr[j] = xn[j];
     }
 #pragma unroll
     for (int j = 0; j < P; ++j) {
@@ -2196,13 +2247,14 @@ static int pick_variant(const ProcArgs &a, int channels, int log2b) {
 template <int LOG2B>
 static hipError_t launch_gw_anchor_t(const ProcArgs &a, int channels, hipStream_t s) {
     constexpr int F = (1 << LOG2B) / 2;
+    constexpr int SL = LOG2B > kMaxLog2Fused ? 256 / FFTCONV_GW_SPLIT : 256;  // slots per workgroup
     static_assert(F % 256 == 0, "a workgroup covers 256 slots");
     const int cls = a.gw_t % kGwP;
     if (channels <= cls || a.gw == nullptr) return hipSuccess;
     ProcArgs args = a;
     args.la_channels = channels;
     const int ny = (channels - cls + kGwP - 1) / kGwP;
-    hipLaunchKernelGGL(gw_anchor_kernel<LOG2B>, dim3(F / 256, ny), dim3(256), 0, s, args);
+    hipLaunchKernelGGL(gw_anchor_kernel<LOG2B>, dim3(F / SL, ny), dim3(256), 0, s, args);
     return hipGetLastError();
 }
 
