@@ -665,8 +665,20 @@ __global__ __launch_bounds__(NT) void lg_cols_inv(LgPass p) {
         // the channel's last workgroup of this pass writes the block state
         __syncthreads();
         if (tid == 0) {
+#ifndef FFTCONV_LG_ARRIVE_RELAXED
+#define FFTCONV_LG_ARRIVE_RELAXED 1
+#endif
+#if FFTCONV_LG_ARRIVE_RELAXED
+            // relaxed: a tile only reports that it has consumed the progress
+            // words and the state (their values were used above); the last
+            // tile reads nothing another tile wrote (the outputs meet the next
+            // launch at the kernel boundary), so no release -- which at agent
+            // scope would write back this XCD's L2 once per tile
+            const int old = __hip_atomic_fetch_add(pg + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
             __threadfence();
             const int old = __hip_atomic_fetch_add(pg + 3, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#endif
             DBG_CHECK(old >= 0 && old < G::NTILE, 55, old, G::NTILE, (int)row, 0);  // (site 55: the arrival counter)
             if (old == G::NTILE - 1) {
                 pg[3] = 0;
