@@ -53,11 +53,12 @@ constexpr int LG_NT = 256;
 constexpr int LG_CNT_WIDE = 1024;
 constexpr int LG_WIDE_MAX_TILES = 512;
 constexpr int LG_E = 4096;  // complex points per column tile (passes A and C), at most
-// tiles per transform, at least (A/B builds: 8 or 16 tiles at B = 16384 --
-// 128..256-byte column runs -- measured 2-20% slower than 4 tiles of 512-byte
-// runs, profiles/r5/r5y_ab_lg_tiles.log)
+// tiles per transform, at least: 8 (B = 16384: 2048-point tiles of 256-byte
+// column runs).  With the per-tile agent-scope release in pass C, 8 or 16
+// tiles were 2-20 % slower than 4 (r5y_ab_lg_tiles.log); without it 8 tiles
+// are 1.4 % faster at lgu and 1.2 % at lgt, 16 slower (r5av_ab_lg_tiles.log)
 #ifndef FFTCONV_LG_TILES
-#define FFTCONV_LG_TILES 1
+#define FFTCONV_LG_TILES 8
 #endif
 
 template <int LM>
