@@ -292,6 +292,7 @@ struct UniformCore {
     // gw_p = the split row (0 = off), gwin = [C][P][B], gw_t = one-block
     // steps so far (the anchor class of the next one)
     bool gw_ok = false;
+    bool narrow = false;  // 2048 <= B <= 8192: 256-thread step workgroups (ProcArgs::narrow)
     int gw_p = 0;
     DevPtr<float2> gwin;
     unsigned long long gw_t = 0;
@@ -629,6 +630,7 @@ struct UniformCore {
             ++la_t;
         }
         lg_fill(a, n);
+        a.narrow = narrow ? 1 : 0;
         a.gw_p = gw_p;  // (every launch: the split order)
         if (gw_p && n == B && gw_windows_allowed()) {
             // a one-block step reads the live windows, then the channels of
@@ -791,6 +793,17 @@ struct TwoStageCore {
     // ev_tail_done: everything of it, its window anchor included (quiesce)
     hipEvent_t ev_main = nullptr, ev_tail = nullptr, ev_tail_done = nullptr;
     bool tail_in_flight = false;
+    int ts_exp = 0;  // (timing probes, FFTCONV_TS_EXP at creation; never in tests)
+    // the tail's step on 256-thread workgroups: 0 never, 1 in periods that ran
+    // as multi-call runs, 2 always (FFTCONV_TAIL_NARROW at creation)
+    int tail_narrow = 2;
+    // the side stream confined to the tail's byte share of the CUs (off: the
+    // tail's step runs on 256-thread workgroups that fit beside the head's,
+    // and a CU-masked side stream held one handle's one-launch-per-call head
+    // launches for 456 us at a time, 21.5-22.9 us per cfg3 call, against
+    // 7.55 unmasked: profiles/r6/r6b, r6c).  FFTCONV_TAIL_MASKED=1 at creation
+    bool tail_masked = false;
+    int run_prio = 0;  // (tuning, FFTCONV_RUN_PRIO at creation: ProcArgs::prio of the runs)
     // tail0 deferred to the end of its period (launch_tail0_flush): the
     // aligned calls' blocks [t0_off, t0_off + t0_n * head_bs) of tail_input
     // still to be convolved by tail_convolver0 (FFTCONV_TAIL0_DEFER=0: off)
@@ -804,6 +817,9 @@ struct TwoStageCore {
     DevPtr<int> t0_err;
     DevPtr<float> t0_ov;
     DevPtr<float2> t0_cv;
+    // [C]: a run's call of this channel wrote no spectrum to t0_xs (its head
+    // buffer out of step with tail_input); the flush recomputes and clears it
+    DevPtr<int> t0_miss;
     Scratch scratch;
     mutable StreamOrder order;
 
@@ -853,7 +869,7 @@ struct TwoStageCore {
         // fraction of the chip's bandwidth (head 512 / IR 200,000: 59.6 us per
         // step on one unit of 32 CUs, 28.7 on 3 units, 21.4 unmasked;
         // profiles/r5/r5d_lgt_tail_units.log)
-        if (tail && ncu >= 8 && !tail->large) {
+        if (tail && ncu >= 8 && !tail->large && tail_masked) {
             // bytes per tail period in B-bin rows: the tail's step (with windows:
             // P-1 near rows of H and X, one window row, and 1/P of an anchor's
             // S H rows, S X rows and P window rows) against T/h head steps
@@ -890,10 +906,20 @@ struct TwoStageCore {
     }
 
     int alloc_buffers() {
+        if (const char *e = getenv("FFTCONV_TS_EXP")) ts_exp = atoi(e);
+        if (const char *e = getenv("FFTCONV_TAIL_NARROW")) tail_narrow = atoi(e);
+        if (const char *e = getenv("FFTCONV_TAIL_MASKED")) tail_masked = atoi(e) != 0;
+        if (const char *e = getenv("FFTCONV_RUN_PRIO")) run_prio = atoi(e);
         if (int r = create_side_stream()) return r;
-        HIP_TRY(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ev_tail_done, hipEventDisableTiming));
+        // The period events order kernels on this device only (no host wait
+        // reads what they guard), so they carry no system-scope fence: with
+        // it, cfg3 one-launch-per-call periods ran at 21.5 us per call on one
+        // box (head launches held for 456 us beside the tail), without it
+        // 6.6 us (profiles/r6/r6b).  (FFTCONV_TS_EXP bit 2: the fence back)
+        const unsigned evf = hipEventDisableTiming | ((ts_exp & 4) ? 0u : hipEventDisableSystemFence);
+        HIP_TRY(hipEventCreateWithFlags(&ev_main, evf));
+        HIP_TRY(hipEventCreateWithFlags(&ev_tail, evf));
+        HIP_TRY(hipEventCreateWithFlags(&ev_tail_done, evf));
         for (auto *b : {&out0, &pre0, &out1, &pre1, &tin_buf[0], &tin_buf[1]}) {
             if (int r = b->alloc(C * T)) return r;
             if (b->n) HIP_TRY(hipMemsetAsync(b->p, 0, b->bytes(), stream));
@@ -911,7 +937,9 @@ struct TwoStageCore {
             if (int r = t0_err.alloc(C)) return r;
             if (int r = t0_ov.alloc(C * head_bs)) return r;
             if (int r = t0_cv.alloc(C * t0_nmax * head_bs)) return r;
+            if (int r = t0_miss.alloc(C)) return r;
             HIP_TRY(hipMemsetAsync(t0_err.p, 0, t0_err.bytes(), stream));
+            if (t0_miss.n) HIP_TRY(hipMemsetAsync(t0_miss.p, 0, t0_miss.bytes(), stream));
         }
         t0_off = t0_n = t0_have = 0;
         return FFTCONV_OK;
@@ -928,6 +956,7 @@ struct TwoStageCore {
         a.act = (int)tail0->S;
         a.n = (int)t0_n; a.nmax = (int)t0_nmax;
         a.k0 = (int)std::min(t0_have, t0_n);
+        a.miss = t0_miss.p;
         HIP_TRY(launch_tail0_flush(tail0->log2b, a, (int)C, s));
         t0_n = t0_have = 0;  // (only once the flush is enqueued: a failed launch keeps the blocks pending)
         return FFTCONV_OK;
@@ -1002,7 +1031,8 @@ struct TwoStageCore {
         std::swap(tail_precalculated, tail_output);                           // :483
         // work after this point reads the swapped-in tail_precalculated: it is
         // the previous period's tail result, so wait for that kernel here
-        if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(s, ev_tail, 0));
+        // (FFTCONV_TS_EXP bit 0, timing probes only: no wait -- racy)
+        if (tail_in_flight && !(ts_exp & 1)) HIP_TRY(hipStreamWaitEvent(s, ev_tail, 0));
         if (tail) {                                                            // :484-485
             hipStream_t ts = period_runs && side_open ? side_open : side;
             HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
@@ -1014,6 +1044,7 @@ struct TwoStageCore {
             // (the next period waits for the tail's output only, not for its
             // window anchor: 19 us of cross-queue wait behind the anchor, r5p;
             // starting the tail before the flush gained nothing, r5s)
+            tail->narrow = (tail_narrow == 2 || (tail_narrow == 1 && period_runs)) && !tail->large;
             if (int r = tail->process_device(tail_input(), T, tail_output, T, T, ts, 0, nullptr, nullptr, ev_tail))
                 return r;
             HIP_TRY(hipEventRecord(ev_tail_done, ts));
@@ -1106,7 +1137,7 @@ struct TwoStageCore {
                                  head->log2b <= kMaxLog2Fused;
             const size_t left = aligned ? (T - tail_input_fill) / head_bs : 0;
             const size_t nrun = std::min(steps - k, left);
-            if (aligned && nrun >= 2 && t0_defer && tail0 && run_supported(head->log2b) && !head->trace_slots &&
+            if (aligned && nrun >= 2 && t0_defer && tail0 && run_supported(head->log2b) &&
                 nrun <= (size_t)INT32_MAX && in_step <= (size_t)LLONG_MAX && out_step <= (size_t)LLONG_MAX) {
                 ProcArgs a{};
                 a.job[0] = head->job(din + k * in_step, is, dout + k * out_step, os, len);  // :417
@@ -1123,6 +1154,12 @@ struct TwoStageCore {
                 if (t0spec) {
                     a.job[0].t0x = t0_xs.p + t0_n * head_bs;
                     a.job[0].t0x_stride = (long long)(t0_nmax * head_bs);
+                    a.job[0].t0m = t0_miss.p;  // (a call that cannot write its spectrum flags the channel)
+                }
+                a.prio = run_prio;
+                if (head->trace_slots) {  // (FFTCONV_PROC_TRACE: the run's last call, per wave)
+                    if (int r = head->trace_fill(a, s)) return r;
+                    ++head->la_t;
                 }
                 RunSteps r{(long long)in_step, (long long)out_step, (int)nrun};
                 HIP_TRY(launch_process_run(head->log2b, a, r, (int)C, s));
@@ -1170,6 +1207,7 @@ struct TwoStageCore {
         precalculated_pos = 0;
         tail_in_flight = false;
         t0_n = t0_have = 0;  // (the deferred blocks' state is reset with everything else)
+        if (t0_miss.n) HIP_TRY(hipMemsetAsync(t0_miss.p, 0, t0_miss.bytes(), stream));
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -1905,7 +1943,10 @@ T *make_or_null(int r, T *p) {
     return p;
 }
 
-hipStream_t pick(void *s, hipStream_t own) { return s ? (hipStream_t)s : own; }
+// A caller's stream argument: NULL is HIP's null (legacy default) stream, as
+// in every HIP API (fftconv.h "Streams"); StreamOrder orders it after the
+// handle's own non-blocking streams, and nothing on it runs ahead of them.
+hipStream_t pick(void *s, hipStream_t) { return (hipStream_t)s; }
 
 }  // namespace
 

@@ -438,7 +438,17 @@ struct RunCarry {
     int par;                // stage buffer holding this call's input (hot)
     const float *next_in;   // the next call's input (null: the run's last call)
     float ov[4];            // overlap samples of the chain's lanes (B <= 256)
+    int4 st;                // the state word the call stored (hot): the next call's, without a reload
 };
+
+// Workgroup barrier for LDS data only: this wave's LDS operations complete,
+// then s_barrier -- unlike __syncthreads, no wait for the wave's outstanding
+// global stores (the pipelined step's chain has just issued its FDL row,
+// tail_input and tail0 spectrum stores; nothing behind this barrier reads
+// them, and the call's closing __syncthreads orders them for the next call).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // ---------------------------------------------------------------------------
 // Pipelined full-block step (2 <= B <= 512): the common call -- one whole
@@ -506,6 +516,9 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
     constexpr bool RH = RUN && Gm::PIPE_EARLY && CNB <= 4;  // (run-carried state: B <= 256)
     float *stage[2] = {ovl, p0l};  // (a run's prefetched input blocks: LDS the step leaves unused)
     const bool hot = RH && rc->hot;
+    // (a run: the state word this step stores when its block succeeds; every
+    // thread holds it, so the next call starts without reloading it)
+    if constexpr (RH) rc->st = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
     if (wave == 0) {
         // ---- critical chain, one wave: R2C, conv, the C2R error check ----
         if (hot) {
@@ -599,8 +612,9 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
     }
     // B1 (B <= 256): every wave at this one barrier -- the chain's share of
     // the next block's pre and its error flag, and the helpers' shares, are
-    // in the reduction slots
-    if constexpr (Gm::PIPE_EARLY) __syncthreads();
+    // in the reduction slots (LDS only: the chain's global stores stay in
+    // flight across it)
+    if constexpr (Gm::PIPE_EARLY) lds_barrier();
     if (wave == 0) {
         // ---- the chain's C2R and overlap-add ----
         wave_sync();
@@ -640,6 +654,7 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
             }
         }
         if (!Gm::PIPE_EARLY && lane == 0) s_err = err ? 1 : 0;
+        proc_stamp(a, 2);  // (timelines: the chain's C2R and overlap-add done)
         if constexpr (Gm::PIPE_EARLY) return !err;
     }
     if constexpr (Gm::PIPE_EARLY) {
@@ -660,6 +675,7 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
         }
         if (ht == 0) J.state[c] = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
         if constexpr (RH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the stage DMA has landed)
+        // (RunCarry::st above is this word)
         proc_stamp(a, 3);
         return true;
     }
@@ -802,6 +818,7 @@ __device__ __forceinline__ bool process_job(const ProcArgs &a, const ProcJob &J,
 
     int processed = 0;
     bool err = false, pre_next = false;
+    bool t0w = false;  // (a run's two-stage head: this call wrote its block's spectrum to t0x)
     for (;;) {
         const bool was_empty = fill == 0;                               // :223
         const int k = min(n - processed, B - fill);                      // :224-227
@@ -893,6 +910,7 @@ __device__ __forceinline__ bool process_job(const ProcArgs &a, const ProcJob &J,
         float2 *Xcur = Xc + (size_t)cur * B;
         // (a run's two-stage head: tail0's copy of a whole block's spectrum)
         float2 *t0r = J.t0x && fill == 0 && k == B ? J.t0x + c * J.t0x_stride : nullptr;
+        t0w = t0w || t0r != nullptr;
         for (int m = tid; m < B; m += NT) {
             const float2 v = real_post<LOG2B, NT>(Z, m, tw);
             Q[m] = v;
@@ -975,6 +993,9 @@ __device__ __forceinline__ bool process_job(const ProcArgs &a, const ProcJob &J,
     }
     // (a live window stays live only across a step that read it and advanced)
     if (tid == 0) J.state[c] = make_int4(cur, act, fill, la_clear(flags, a) | (gwin && !err ? FLAG_GW : 0));
+    // a run's call whose head buffer is out of step with tail_input wrote no
+    // spectrum for tail0's pending block: the flush recomputes this channel's
+    if (J.t0x && !t0w && tid == 0) J.t0m[c] = 1;
     if (epi && (!one_block || err)) twostage_epilogue<NT>(J, c, outc, inc, n);
     proc_stamp(a, 3);
     return false;
@@ -1178,9 +1199,16 @@ __global__ __launch_bounds__(NT, 2) void upols_run_kernel(ProcArgs a, RunSteps r
     const size_t c = blockIdx.x;
     ProcJob J = a.job[0];
     RunCarry rc{};
+    // (issue priority over the waves of other kernels on the same SIMD: the
+    // two-stage tail beside the run; 1 = the chain wave, 2 = every wave)
+    if (a.prio == 2 || (a.prio == 1 && threadIdx.x < 64)) __builtin_amdgcn_s_setprio(3);
+    unsigned t0 = 0;
     for (int k = 0; k < r.n; ++k) {
+        if (a.la_trace && k == r.n - 1) t0 = (unsigned)__builtin_amdgcn_s_memrealtime();  // (the last call's start)
         rc.next_in = k + 1 < r.n ? J.in + r.in_step : nullptr;
-        const bool kept = process_job<LOG2B, NT, false, NTL, true>(a, J, c, J.state[c], smem, &rc);
+        // (a hot call's state word is the one the previous call stored)
+        const int4 st = rc.hot ? rc.st : J.state[c];
+        const bool kept = process_job<LOG2B, NT, false, NTL, true>(a, J, c, st, smem, &rc);
         rc.hot = kept && rc.next_in != nullptr;  // (the next call's block is in stage[par ^ 1])
         rc.par ^= 1;
         __syncthreads();
@@ -1190,6 +1218,16 @@ __global__ __launch_bounds__(NT, 2) void upols_run_kernel(ProcArgs a, RunSteps r
         if (J.add1) J.add1 += J.n;
         if (J.tin) J.tin += J.n;
         if (J.t0x) J.t0x += J.n;
+    }
+    if (a.la_trace && (threadIdx.x >> 6) < 4 && (threadIdx.x & 63) == 0) {
+        // launch timeline (FFTCONV_PROC_TRACE, tuning): the run's last call,
+        // role 6 as upols_process_kernel's record (the phase stamps are that call's)
+        const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
+        const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID
+        const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+        const int wave = (int)(threadIdx.x >> 6);
+        a.la_trace[(size_t)blockIdx.x * 4 + wave] =
+            make_int4(6 | (wave << 4), (int)((hw & 0xffffu) | ((xcc & 0xffu) << 24)), (int)t0, (int)t1);
     }
 }
 
@@ -1801,7 +1839,10 @@ __global__ __launch_bounds__(64) void tail0_r2c_kernel(Tail0Args t) {
     float2 *bufA = reinterpret_cast<float2 *>(smem), *bufB = bufA + B, *twl = bufB + B;
     const ProcJob &J = t.pa.job[0];
     const size_t c = blockIdx.x;
-    const int k = t.k0 + (int)blockIdx.y, lane = threadIdx.x;
+    // grid.y: every pending block; blocks [0, k0) have their spectra from the
+    // head's run unless the run missed some of this channel's (t.miss)
+    const int k = (int)blockIdx.y, lane = threadIdx.x;
+    if (k < t.k0 && !t.miss[c]) return;
     dma_f32<64>(reinterpret_cast<float *>(bufA), J.in + c * J.in_stride + (size_t)k * B, B);  // packed z[0..B/2)
     for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);              // the padding half
     dma_16b<64>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
@@ -1999,6 +2040,7 @@ __global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_replay_kernel(Tail0Args 
     const ProcJob &J = t.pa.job[0];
     const size_t c = blockIdx.x;
     const int n = t.n;
+    if (threadIdx.x == 0) t.miss[c] = 0;  // (every pending spectrum was recomputed or is the run's)
     if (!t.err[c]) {
         if (threadIdx.x == 0) {
             const int4 st = J.state[c];
@@ -2024,35 +2066,48 @@ __global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_replay_kernel(Tail0Args 
 }
 
 // The whole flush in ONE launch at B = 64 (cfg3's head; one slot chunk per
-// channel): per channel workgroup, (1) the pending blocks' R2C by the four
-// waves into the LDS X rows, (2) the MAC of tail0_mac_kernel, (3) each
-// block's C2R, (4) overlap-add, overlap save, the FDL rows and the state --
-// or, if a block's conv slot 0 is not finite, the block-by-block replay of
-// tail0_replay_kernel.  The same arithmetic in the same order as the five
-// kernels (bit-identical); the spectra, convs and C2R outputs stay in LDS.
-// LDS: [H rows + zero | X rows (q >= -1) + zero rows] (the C2R outputs
-// reuse the H rows once the MAC is done) | tw | 4 x 2 B-point FFT buffers |
-// conv rows (the inputs before the MAC) | overlap | flag
+// channel), the default there: per channel workgroup
+//   (0) every row by LDS-DMA: tail0's IR rows, the previous period's FDL rows,
+//       the pending spectra the head's run wrote (blocks [0, k0)), the
+//       overlap, and the inputs of the blocks still to transform;
+//   (1) the R2C of blocks [r0, n) (r0 = k0, or 0 if the run missed some of
+//       this channel's spectra) into their LDS X rows;
+//   (2) the MAC of tail0_mac_kernel, conv rows to LDS;
+//   (3) each block's C2R and realfft's error check;
+//   (4) overlap-add, overlap save, the FDL rows and the state -- or, if a
+//       block's conv slot 0 is not finite, the block-by-block replay of
+//       tail0_replay_kernel.
+// The same arithmetic in the same order as the five kernels (bit-identical).
+// The B = 64 transforms use 16 of a wave's 64 lanes (16 radix-4 butterflies
+// per stage), so each wave runs FOUR blocks' transforms at once, one per
+// 16-lane group, each in its own LDS buffers: the same butterflies per lane
+// group, a quarter of the passes (the r4 fused kernel ran them one at a time,
+// 16 per wave: 46 us per flush; the five kernels beside the tail's anchor,
+// 81 us per cfg3 period, profiles/r5/r5ai).
+// LDS: [H rows + zero | X rows (q >= -1) + zero rows] (the C2R outputs reuse
+// the H rows once the MAC is done) | tw | 16 groups x 2 B-point buffers |
+// conv rows (the inputs to transform before the MAC) | overlap | flag
+constexpr int T0F_G = 16;  // lane groups per workgroup (4 waves x 4): transforms per pass
 template <int LOG2B>
 __host__ __device__ constexpr size_t tail0_fused_lds(int act, int n) {
     constexpr size_t B = (size_t)1 << LOG2B;
-    return tail0_mac_lds<LOG2B>(act, n) + 2 * B * 8 + 4 * 2 * B * 8 + (size_t)n * (B / 2) * 16 + B * 4 + 16;
+    return tail0_mac_lds<LOG2B>(act, n) + 2 * B * 8 + T0F_G * 2 * B * 8 + (size_t)n * (B / 2) * 16 + B * 4 + 16;
 }
 template <int LOG2B>
 __host__ __device__ constexpr bool tail0_fused_fits(int act, int n) {
-    constexpr size_t B = (size_t)1 << LOG2B;
-    return LOG2B == 6 && n <= (256 / T0_FC) * T0_J && tail0_fused_lds<LOG2B>(act, n) <= 160 * 1024 &&
-           (size_t)(act + 1) * T0_FC * 16 >= (size_t)n * 2 * B * 4;
+    return LOG2B == 6 && act >= 1 && n >= 1 && n <= (256 / T0_FC) * T0_J && n <= act + 1 &&
+           tail0_fused_lds<LOG2B>(act, n) <= 160 * 1024;
 }
 template <int LOG2B>
 __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
-    constexpr int B = 1 << LOG2B, F = B / 2, FC = T0_FC, J = T0_J, RS = J + 1, NT = 256;
-    static_assert(F == FC, "one slot chunk per channel (B = 64)");
+    constexpr int B = 1 << LOG2B, F = B / 2, FC = T0_FC, J = T0_J, RS = J + 1, NT = 256, GL = 16;
+    static_assert(F == FC && B / 4 == GL, "one slot chunk per channel, 16 butterflies per stage (B = 64)");
     constexpr float invN = 1.0f / (float)(2 * B);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const ProcJob &J0 = t.pa.job[0];
     const size_t c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = wave * 4 + (lane >> 4), gl = lane & 15;  // this lane's transform group, its lane in it
     const int4 st = J0.state[c];
     const int cur0 = st.x, act = st.y, n = t.n;
     const size_t rows = (size_t)J0.S * B;
@@ -2060,17 +2115,19 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
     float4 *Xs = Hs + (size_t)(t.act + 2) * FC;       // Xs[q * FC], q >= -1
     unsigned char *rest = smem + tail0_mac_lds<LOG2B>(t.act, n);
     float2 *twl = reinterpret_cast<float2 *>(rest);
-    float2 *wb = twl + 2 * B;                          // [4 waves][2][B]
-    float4 *cvs = reinterpret_cast<float4 *>(wb + 4 * 2 * B);  // [n][F]
-    float *ins = reinterpret_cast<float *>(cvs);       // [n][B] inputs, before the MAC
+    float2 *gA = twl + 2 * B + (size_t)grp * 2 * B, *gB = gA + B;  // this group's transform buffers
+    float4 *cvs = reinterpret_cast<float4 *>(twl + 2 * B + (size_t)T0F_G * 2 * B);  // [n][F]
+    float *ins = reinterpret_cast<float *>(cvs);       // [n][B] inputs to transform, before the MAC
     float *ovs = reinterpret_cast<float *>(cvs + (size_t)n * F);
     int &s_err = *reinterpret_cast<int *>(ovs + B);
     float *ys = reinterpret_cast<float *>(smem);       // [n][2B], over the H rows after the MAC
     const bool geo = act == t.act;  // (not the geometry the LDS was sized for: replay)
+    const int r0 = t.miss[c] ? 0 : min(t.k0, n);      // blocks [r0, n) are transformed here
 
-    // ---- prologue: every row by LDS-DMA (no VGPRs, all in flight) ----
+    // ---- (0) every row by LDS-DMA (no VGPRs, all in flight) ----
     const float4 *H = reinterpret_cast<const float4 *>(J0.H + c * rows);
     const float4 *X = reinterpret_cast<const float4 *>(J0.X + c * rows);
+    const float4 *xs = reinterpret_cast<const float4 *>(t.xs + (size_t)c * t.nmax * B);
     const int nq = act - 1 + n;
     if (tid == 0) s_err = geo ? 0 : 1;
     if (geo) {
@@ -2084,33 +2141,43 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
             if (r2 + half < act)
                 __builtin_amdgcn_global_load_lds((gptr_t)(H + (size_t)(r2 + half) * F + f),
                                                  (lptr_t)(Hs + (size_t)r2 * FC), 16, 0, 0);
-        for (int r2 = wave * 2; r2 < act - 1; r2 += 8) {  // the previous period's FDL rows
+        // X rows q < act - 1 + r0: the previous period's FDL rows, then the
+        // spectra of pending blocks [0, r0) (the run's)
+        for (int r2 = wave * 2; r2 < act - 1 + r0; r2 += 8) {
             const int q = r2 + half;
-            int r = cur0 + act - 1 - q;
-            if (r >= act) r -= act;
-            if (q < act - 1)
-                __builtin_amdgcn_global_load_lds((gptr_t)(X + (size_t)r * F + f), (lptr_t)(Xs + (size_t)r2 * FC), 16,
-                                                 0, 0);
+            const float4 *src;
+            if (q < act - 1) {
+                int r = cur0 + act - 1 - q;
+                if (r >= act) r -= act;
+                src = X + (size_t)r * F;
+            } else {
+                src = xs + (size_t)(q - (act - 1)) * F;
+            }
+            if (q < act - 1 + r0)
+                __builtin_amdgcn_global_load_lds((gptr_t)(src + f), (lptr_t)(Xs + (size_t)r2 * FC), 16, 0, 0);
         }
         dma_16b<NT>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
         dma_f32<NT>(ovs, J0.overlap + c * B, B);
-        for (int k = wave; k < n; k += 4)  // (tail_input blocks: the job's input, stride T)
+        for (int k = r0 + wave; k < n; k += 4)  // (tail_input blocks: the job's input, stride T)
             dma_f32<64>(ins + (size_t)k * B, J0.in + c * J0.in_stride + (size_t)k * B, B);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (!geo) goto replay;
     {
-        // ---- (1) R2C of each pending block (:229-241) into its X row ----
-        float2 *bA = wb + (size_t)wave * 2 * B, *bB = bA + B;
-        for (int k = wave; k < n; k += 4) {
-            for (int m = lane; m < B; m += 64)
-                bA[m] = m < B / 2 ? make_float2(ins[(size_t)k * B + 2 * m], ins[(size_t)k * B + 2 * m + 1])
-                                  : make_float2(0.f, 0.f);
+        // ---- (1) R2C of blocks [r0, n) (:229-241) into their X rows, 16 at a time ----
+        for (int k0 = r0; k0 < n; k0 += T0F_G) {
+            const int k = k0 + grp;
+            const bool live = k < n;
+            for (int m = gl; m < B; m += GL)
+                gA[m] = live && m < B / 2 ? make_float2(ins[(size_t)k * B + 2 * m], ins[(size_t)k * B + 2 * m + 1])
+                                          : make_float2(0.f, 0.f);
             wave_sync();
-            float2 *Z = lds_cfft<LOG2B, 64, false, true>(bA, bB, twl);
-            float2 *xr = reinterpret_cast<float2 *>(Xs + (size_t)(k + act - 1) * FC);
-            for (int m = lane; m < B; m += 64) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
+            float2 *Z = lds_cfft<LOG2B, GL, false, true>(gA, gB, twl);
+            if (live) {
+                float2 *xr = reinterpret_cast<float2 *>(Xs + (size_t)(k + act - 1) * FC);
+                for (int m = gl; m < B; m += GL) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
+            }
             wave_sync();
         }
         __syncthreads();
@@ -2149,15 +2216,19 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
             }
         }
         __syncthreads();
-        // ---- (3) each block's C2R (realfft's error: a non-finite DC / Nyquist) ----
-        for (int k = wave; k < n; k += 4) {
-            const float2 *Zc = reinterpret_cast<const float2 *>(cvs + (size_t)k * F);
-            if (lane == 0 && !(isfinite(Zc[0].x) && isfinite(Zc[0].y))) s_err = 1;
-            for (int m = lane; m < B; m += 64) bA[m] = real_pre<LOG2B, 64>(Zc, m, twl);
+        // ---- (3) each block's C2R, 16 at a time (realfft's error: a non-finite DC / Nyquist) ----
+        for (int k0 = 0; k0 < n; k0 += T0F_G) {
+            const int k = k0 + grp;
+            const bool live = k < n;
+            const float2 *Zc = reinterpret_cast<const float2 *>(cvs + (size_t)min(k, n - 1) * F);
+            if (live && gl == 0 && !(isfinite(Zc[0].x) && isfinite(Zc[0].y))) s_err = 1;
+            for (int m = gl; m < B; m += GL) gA[m] = real_pre<LOG2B, 64>(Zc, m, twl);
             wave_sync();
-            const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, 64, true, true>(bA, bB, twl));
-            float *yr = ys + (size_t)k * 2 * B;
-            for (int j = lane; j < 2 * B; j += 64) yr[j] = y[j];
+            const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, GL, true, true>(gA, gB, twl));
+            if (live) {
+                float *yr = ys + (size_t)k * 2 * B;
+                for (int j = gl; j < 2 * B; j += GL) yr[j] = y[j];
+            }
             wave_sync();
         }
         __syncthreads();
@@ -2185,12 +2256,14 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
             if (cur < 0) cur += act;
             const int flags = (st.w & ~(FLAG_PRE | FLAG_INBUF)) ^ ((n & 1) ? FLAG_REV : 0);
             J0.state[c] = make_int4(cur, act, 0, la_clear(flags, t.pa));
+            t.miss[c] = 0;
         }
         return;
     }
 replay:
     // tail_convolver0.process block by block from the untouched state (the
     // FDL, the overlap and the state word are not written above)
+    if (tid == 0) t.miss[c] = 0;
     for (int k = 0; k < n; ++k) {
         ProcJob Jk = J0;
         Jk.in = J0.in + (size_t)k * B;
@@ -2279,8 +2352,46 @@ hipError_t launch_gw_anchor(int log2b, const ProcArgs &a, int channels, hipStrea
 
 bool gw_supported(int log2b, int S) { return log2b >= 10 && log2b <= kMaxLog2Block && S >= 3 * kGwP; }
 
+// The generic step on 256 threads for 2048 <= B <= 8192 (ProcArgs::narrow):
+// one wave per SIMD and up to 512 VGPRs, so that the workgroup fits a CU
+// beside a multi-call run's workgroup (4 waves of ~208 VGPRs) -- the
+// 512-thread kernel's 2 waves per SIMD of ~200 VGPRs do not, and the cfg3
+// tail then waited for the few CUs the run left free (227 us per period
+// beside the run vs 44 us alone, profiles/r5/r5ai).  The MAC keeps each
+// slot's row order and the transforms the same butterflies: same bits.
+template <int LOG2B, bool ZZ, bool NTL>
+__global__ __launch_bounds__(256, 1) void upols_narrow_kernel(ProcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const size_t c = blockIdx.x;
+    const ProcJob &J = a.job[blockIdx.y];
+    process_job<LOG2B, 256, ZZ, NTL>(a, J, c, J.state[c], smem);
+}
+
 template <int LOG2B>
 static hipError_t launch_process_t(const ProcArgs &a, int channels, hipStream_t s) {
+    if constexpr (LOG2B >= 11 && LOG2B <= kMaxLog2Fused) {
+        if (a.narrow) {
+            using Gn = Geo<LOG2B, 256>;
+            auto kern = upols_narrow_kernel<LOG2B, false, false>;
+            const int var = pick_variant(a, channels, LOG2B);
+            ProcArgs args = a;
+            args.pipe = 0;
+            args.lag = pipeline_lag(LOG2B);
+            switch (var & 3) {
+                case 1: kern = upols_narrow_kernel<LOG2B, true, false>; break;
+                case 2: kern = upols_narrow_kernel<LOG2B, false, true>; break;
+                case 3: kern = upols_narrow_kernel<LOG2B, true, true>; break;
+                default: break;
+            }
+            if (Gn::lds_bytes > 64 * 1024) {
+                hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)Gn::lds_bytes);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(kern, dim3(channels, a.njobs), dim3(256), Gn::lds_bytes, s, args);
+            return hipGetLastError();
+        }
+    }
     constexpr int PNT = proc_nt(LOG2B);
     using Gm = Geo<LOG2B, PNT>;
     auto kern = upols_process_kernel<LOG2B, PNT, false, false>;
@@ -2361,9 +2472,8 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
             if (e != hipSuccess) return e;
         }
         if constexpr (LOG2B == 6) {
-            // (opt-in: one kernel flushes faster alone, 46 vs 55 us, but the
-            // cfg3 step beside the tail is slower, 7.54 vs 7.17 us, r4v A/B)
-            if (tail0_fused_fits<LOG2B>(a.act, a.n) && g_variant != VARIANT_AUTO && (g_variant & VARIANT_T0FUSED)) {
+            // (VARIANT_T0FUSED: the five kernels instead, bit-identical)
+            if (tail0_fused_fits<LOG2B>(a.act, a.n) && !(g_variant != VARIANT_AUTO && (g_variant & VARIANT_T0FUSED))) {
                 const size_t fl = tail0_fused_lds<LOG2B>(a.act, a.n);
                 auto fk = tail0_fused_kernel<LOG2B>;
                 if (hipError_t e = hipFuncSetAttribute((const void *)fk, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2377,9 +2487,8 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
         // (blocks [0, k0) have their spectra from the head's run; the overlap
         // copy tail0_r2c makes at block 0 is then tail0_mac's)
         if (t.k0 < 0 || t.k0 > a.n) return hipErrorInvalidValue;
-        if (t.k0 < a.n)
-            hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n - t.k0), dim3(64), 4 * B * sizeof(float2),
-                               s, t);
+        // (always: with k0 == n its workgroups only test the channel's miss flag)
+        hipLaunchKernelGGL(tail0_r2c_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
         hipLaunchKernelGGL(mk, dim3(channels, F / FC), dim3(256), lds, s, t);
         hipLaunchKernelGGL(tail0_c2r_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
         hipLaunchKernelGGL(tail0_commit_kernel<LOG2B>, dim3(channels, (a.n + KT - 1) / KT), dim3(256), 0, s, t);

@@ -64,7 +64,7 @@ enum : int {
     VARIANT_NOFMIX = 64,  // crossfade on the lookahead step: stand-alone mix kernel instead of B's epilogue
     VARIANT_IRBLOCK = 128,  // IR transforms: one segment per workgroup (else one per wave, 64 <= B <= 1024)
     VARIANT_T0BLOCK = 256,  // two-stage: tail0 per block (else deferred to the end of its period), read at create
-    VARIANT_T0FUSED = 512,  // deferred tail0 at B = 64: one fused flush kernel instead of five (bit-identical)
+    VARIANT_T0FUSED = 512,  // deferred tail0 at B = 64: the five-kernel flush instead of the fused one (bit-identical)
     VARIANT_NOGW = 1024,    // B >= 1024: no far-row windows, every step sums its far rows itself (tests)
     VARIANT_NORUN = 2048,   // process_device_steps: one launch per call (else a run of a period's calls per launch)
     VARIANT_AUTO = 0x7fffffff
@@ -111,6 +111,11 @@ struct ProcJob {
     // the period's flush skips those blocks' transforms; null = none
     float2 *t0x;
     long long t0x_stride;
+    // [C]: set by a run's call that did NOT write its block's spectrum to t0x
+    // (a channel whose head buffer is out of step with tail_input, e.g. after
+    // a C2R error on a partial call, :264-267): the flush recomputes that
+    // channel's pending spectra from tail_input and clears the flag
+    int *t0m;
 };
 
 // Twiddle tables of the long-block path (large.hip), f64-rounded f32:
@@ -190,6 +195,13 @@ struct ProcArgs {
     float2 *gw;
     int gw_p;
     int gw_t;
+    // 2048 <= B <= 8192: 256-thread workgroups (upols_narrow_kernel) instead
+    // of 512 -- a two-stage tail beside the head's multi-call run, so one
+    // tail workgroup fits each CU next to a run workgroup (same bits)
+    int narrow;
+    // multi-call run (upols_run_kernel): the waves' issue priority (s_setprio;
+    // 0 = the default) -- the latency-bound chain beside the two-stage tail
+    int prio;
 };
 
 struct IrArgs {
@@ -296,6 +308,7 @@ struct Tail0Args {
     int n;                 // pending blocks
     int nmax;              // row pitch of xs / ys in blocks
     int k0;                // blocks [0, k0) already have their spectra in xs (the head's run wrote them)
+    int *miss;             // [C]: 1 = the run missed some of this channel's spectra: recompute [0, n) (ProcJob::t0m)
 };
 bool tail0_defer_supported(int log2b, int act, int nmax);
 bool tail0_defer_allowed();  // VARIANT_T0BLOCK unset

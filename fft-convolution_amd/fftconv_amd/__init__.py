@@ -10,7 +10,8 @@ Every object is a batch of `channels` independent convolvers on one GPU
 (channels=1 is exactly one reference instance).  Host arrays are
 [channels][samples] (1-D for a single channel).  `process_device` takes raw
 device pointers (e.g. torch tensors' data_ptr()) and a HIP stream and is
-asynchronous.
+asynchronous.  Stream 0 is HIP's null stream -- torch's default stream --
+as everywhere in HIP: work enqueued there after a call sees its results.
 
 A reference panic surfaces as `ConvolutionPanic`; HIP failures as
 `DeviceError`.  There is no CPU fallback: importing works anywhere, but
@@ -298,17 +299,17 @@ class _Base:
         _check(self._fn("synchronize")(self._h))
 
     def process_device(self, d_in: int, in_stride: int, d_out: int, out_stride: int, n: int, stream: int = 0):
-        """process() on device buffers, enqueued on `stream`.  stream 0 selects the
-        handle's own stream (fftconv.h), NOT the default HIP stream: torch's
-        default stream (cuda_stream == 0) does not wait for it -- pass an explicit
-        stream, or synchronize() the handle before reading the output."""
+        """process() on device buffers, enqueued on `stream` (0 = HIP's null
+        stream, torch's default stream; fftconv.h "Streams"): ordered after the
+        handle's previous work, and work enqueued on `stream` afterwards sees
+        the output."""
         _check(self._fn("process_device")(self._h, C.c_void_p(d_in), in_stride, C.c_void_p(d_out), out_stride, n,
                                           C.c_void_p(stream) if stream else None))
 
     def process_device_steps(self, d_in: int, in_stride: int, in_step: int, d_out: int, out_stride: int,
                              out_step: int, n: int, steps: int, stream: int = 0):
         """`steps` consecutive process_device calls (offsets in floats); stream 0 =
-        the handle's own stream, as process_device."""
+        HIP's null stream, as process_device."""
         _check(self._fn("process_device_steps")(self._h, C.c_void_p(d_in), in_stride, in_step, C.c_void_p(d_out),
                                                 out_stride, out_step, n, steps,
                                                 C.c_void_p(stream) if stream else None))

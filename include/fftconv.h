@@ -27,6 +27,15 @@
  *
  * There is no CPU fallback: creating a handle without a usable gfx950 device
  * fails with FFTCONV_E_DEVICE.
+ *
+ * Streams: every `void *hip_stream` argument is a hipStream_t, and NULL is
+ * HIP's null (legacy default) stream -- the same meaning it has in every HIP
+ * API and the stream PyTorch's default stream maps to.  A call enqueued on a
+ * stream is ordered after the handle's previous work wherever that ran (one
+ * event wait when the stream differs from the last one used), and anything
+ * enqueued on the same stream afterwards sees its results.  Host-synchronous
+ * entry points use the handle's own (non-blocking) stream and wait for it;
+ * *_synchronize waits for all of a handle's work.
  */
 #ifndef FFTCONV_H
 #define FFTCONV_H
@@ -81,7 +90,7 @@ size_t fftconv_compute_tail_block_size(size_t head_len, size_t response_len); /*
  * part; the transform runs with those parts as 0).  Such a row is NOT divided
  * by n: Fft::inverse returns the error through `?` (:42) before its
  * normalisation loop (:44-46).  Strides in floats; enqueued on `hip_stream`
- * (NULL = legacy stream). */
+ * (NULL = HIP's null stream). */
 int fftconv_fft_forward(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
                         size_t out_stride, void *hip_stream);
 int fftconv_fft_inverse(int device, size_t n, size_t rows, const float *d_in, size_t in_stride, float *d_out,
@@ -172,7 +181,7 @@ int fftconv_uniform_update_channel(fftconv_uniform *h, size_t channel, const flo
                                    size_t response_len);
 /* update() from device-resident responses (channel c at d_responses[c*stride],
  * stride 0 = one response for every channel), enqueued on `hip_stream`
- * (NULL = own stream) without a host synchronisation or an allocation. */
+ * (NULL = HIP's null stream) without a host synchronisation or an allocation. */
 int fftconv_uniform_update_device(fftconv_uniform *h, const float *d_responses, size_t response_len,
                                   size_t response_stride, void *hip_stream);
 /* FFTConvolver::reset, src/fft_convolver.rs:296-306 (all channels). */
@@ -183,8 +192,8 @@ int fftconv_uniform_reset(fftconv_uniform *h);
  * FFTCONV_E_INVALID like the reference's slice panic).  Synchronous. */
 int fftconv_uniform_process(fftconv_uniform *h, const float *input, size_t input_len,
                             float *output, size_t output_len);
-/* Same on device-resident buffers, enqueued on `hip_stream` (NULL = the
- * handle's own stream), asynchronous: channel c reads d_input[c*in_stride ..
+/* Same on device-resident buffers, enqueued on `hip_stream` (NULL = HIP's
+ * null stream), asynchronous: channel c reads d_input[c*in_stride ..
  * + len] and writes d_output[c*out_stride .. + len]. */
 int fftconv_uniform_process_device(fftconv_uniform *h, const float *d_input, size_t in_stride,
                                    float *d_output, size_t out_stride, size_t len, void *hip_stream);

@@ -196,7 +196,7 @@ impl GpuCrossfadeTwoStageConvolver {
 
 /// A batch of independent FFTConvolver channels on one GPU (the throughput
 /// path): responses and blocks are channel-major, device pointers are HBM
-/// resident, work is queued on `stream` (a hipStream_t, null = the batch's own).
+/// resident, work is queued on `stream` (a hipStream_t, null = HIP's null stream).
 pub struct GpuFFTConvolverBatch {
     h: NonNull<ffi::fftconv_uniform>,
 }

@@ -47,8 +47,9 @@ def summarise(path):
                 m = (role == k) & ((wave >= nchain) == (w == 2))
                 for q in range(4):
                     mm = m & (st[:, q] != 0)
-                    if mm.any():
-                        ph.setdefault((int(k), w, q), []).append(np.median(st[mm, q] - base))
+                    if mm.any():  # (relative to each wave's own start: a run's last call)
+                        own = r[mm, 2].astype(np.int64) & 0xffffffff
+                        ph.setdefault((int(k), w, q), []).append(np.median(st[mm, q] - own))
             m = role == k
             d = per_role.setdefault(int(k), {"n": [], "start": [], "end": [], "dur": []})
             d["n"].append(int(m.sum()))

@@ -31,12 +31,11 @@ from fftconv_amd import shard  # noqa: E402
 def run(conv, d_in, in_stride, in_step, C, B, NB):
     dev = torch.device("cuda:0")
     yd = torch.empty(NB, C, B, device=dev)
-    # an explicit stream, ordered after the default stream's work: stream 0 would
-    # select the handle's own stream (fftconv.h), which the default stream does not wait for
-    s = torch.cuda.Stream(dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    conv.process_device_steps(d_in.data_ptr(), in_stride, in_step, yd.data_ptr(), B, C * B, B, NB, s.cuda_stream)
-    s.synchronize()
+    # stream 0 = HIP's null stream, torch's default stream (fftconv.h
+    # "Streams"): the read below is ordered after every launch with no explicit
+    # synchronisation -- the pattern that raced while 0 meant the handle's own
+    # stream (round 5)
+    conv.process_device_steps(d_in.data_ptr(), in_stride, in_step, yd.data_ptr(), B, C * B, B, NB, 0)
     return yd.cpu().numpy()
 
 

@@ -71,8 +71,7 @@ def test_cfg4_eight_ranks_full_size(amd, oracle_mod, tmp_path):
             dry = np.broadcast_to(shard.synth_shared_dry(NB, B)[:, None, :], (NB, total, B))
             d_in, in_stride = torch.from_numpy(shard.synth_shared_dry(NB, B)).to(dev), 0
         yd = torch.empty(NB, total, B, device=dev)
-        # an explicit stream, ordered after the default stream's work: stream 0 would
-        # select the handle's own stream (fftconv.h), which the default stream does not wait for
+        # an explicit stream here (the ranks use stream 0, the null stream)
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         conv.process_device_steps(d_in.data_ptr(), in_stride, in_stride * total if in_stride else B, yd.data_ptr(), B,

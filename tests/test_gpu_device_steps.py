@@ -77,3 +77,65 @@ def test_twostage_device_steps(amd, oracle_mod, head, L):
         assert np.array_equal(np.isnan(y[c]), np.isnan(r)), c
         m = ~np.isnan(r)
         assert_close(y[c][m], r[m], what=f"channel {c}")
+
+
+NORUN = 2048  # VARIANT_NORUN: process_device_steps launches once per call
+
+
+@pytest.mark.parametrize("head,L", [(64, 20000), (128, 40000)])
+def test_twostage_run_after_nan_partial_call(amd, oracle_mod, head, L):
+    """a C2R error on a partial call freezes the head's fill
+    (src/fft_convolver.rs:264-267) while tail_input_fill advances, so the
+    head's buffer is out of step with tail0's blocks: the run's calls of that
+    channel cannot write tail0's pending spectra, flag the channel, and the
+    flush recomputes them.  Two half calls (a NaN in channel 1's first) then
+    aligned process_device_steps over more than two tail periods: bitwise
+    equal to one launch per call (VARIANT_NORUN), and the oracle."""
+    rng = np.random.default_rng(830 + head)
+    C = 3
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    half = [np.stack([white(rng, head // 2) for _ in range(C)]) for _ in range(2)]
+    half[0][1, 5] = np.nan
+    outs = []
+    for v in (-1, NORUN):
+        amd.set_kernel_variant(v)
+        try:
+            conv = amd.TwoStageFFTConvolver.init(hs, head, L, channels=C)
+            T = conv.tail_block_size
+            K = 2 * T // head + 7
+            x = np.stack([white(np.random.default_rng(831 + head), K * head) for _ in range(C)])
+            pre = np.concatenate([conv.process(h) for h in half], axis=1)
+            outs.append(np.concatenate([pre, _device_steps(conv, x, head, K)], axis=1))
+        finally:
+            amd.set_kernel_variant(-1)
+    assert np.array_equal(outs[0], outs[1], equal_nan=True)
+    for c in range(C):
+        ref = oracle_mod.TwoStageFFTConvolver.init(hs[c], head, L)
+        r = np.concatenate([ref.process(h[c]) for h in half] +
+                           [ref.process(x[c, k * head:(k + 1) * head]) for k in range(K)])
+        assert np.array_equal(np.isnan(outs[0][c]), np.isnan(r)), c
+        m = ~np.isnan(r)
+        assert_close(outs[0][c][m], r[m], what=f"channel {c}")
+
+
+@pytest.mark.parametrize("head,L", [(64, 40000), (64, 100000), (128, 300000)])
+def test_twostage_narrow_tail_bitwise(amd, monkeypatch, head, L):
+    """The T-block tail's step on 256-thread workgroups (ProcArgs::narrow,
+    upols_narrow_kernel; T = 2048 / 4096 / 8192) is bit-identical to the
+    512-thread kernel: aligned process_device_steps over three tail periods,
+    FFTCONV_TAIL_NARROW=2 (every period) against 0, with a NaN block."""
+    rng = np.random.default_rng(840 + head + L)
+    C = 4
+    hs = np.stack([ir(rng, L) for _ in range(C)])
+    outs = []
+    for nar in ("2", "0"):
+        monkeypatch.setenv("FFTCONV_TAIL_NARROW", nar)
+        conv = amd.TwoStageFFTConvolver.init(hs, head, L, channels=C)
+        monkeypatch.delenv("FFTCONV_TAIL_NARROW")
+        T = conv.tail_block_size
+        K = 3 * T // head + 3
+        x = np.stack([white(np.random.default_rng(841), K * head) for _ in range(C)])
+        x[2, (T // head + 1) * head + 3] = np.nan
+        outs.append(_device_steps(conv, x, head, K))
+    assert np.isfinite(outs[0][0]).all()
+    assert np.array_equal(outs[0], outs[1], equal_nan=True)

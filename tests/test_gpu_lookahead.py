@@ -206,24 +206,46 @@ def test_lookahead_windows_never_read_unwritten(amd, monkeypatch, C, B):
         assert np.array_equal(y, outs[0])
 
 
-def test_device_stream_zero_is_the_handle_stream(amd):
-    """stream 0 selects the handle's own stream (fftconv.h), not the default
-    HIP stream: after synchronize() the output is complete and equals the
-    same calls on an explicit stream."""
+def test_device_stream_zero_is_the_null_stream(amd, oracle_mod):
+    """stream 0 is HIP's null stream -- torch's default stream (fftconv.h
+    "Streams"): process_device_steps(..., 0) issued from the default stream,
+    then .cpu() on that stream with no synchronize() in between, sees every
+    call's output; it equals the same calls on an explicit stream and the
+    oracle.  (Until round 5, 0 selected the handle's own non-blocking stream,
+    and this read raced the last launches: the cfg4 test's failure.)"""
     import torch
 
     rng = np.random.default_rng(380)
-    C, B, L, K = 16, 256, 48 * 256, 64
+    C, B, L, K = 16, 256, 48 * 256, 96
     hs = np.stack([ir(rng, L) for _ in range(C)])
-    xd = torch.from_numpy(np.stack([white(rng, C * B).reshape(C, B) for _ in range(K)])).to("cuda:0")
+    x = np.stack([white(rng, C * B).reshape(C, B) for _ in range(K)])  # [K][C][B]
+    xd = torch.from_numpy(x).to("cuda:0")
+    assert torch.cuda.current_stream().cuda_stream == 0
     a, b = amd.FFTConvolver.init(hs, B, L, channels=C), amd.FFTConvolver.init(hs, B, L, channels=C)
-    ya, yb = torch.empty_like(xd), torch.empty_like(xd)
+    ya = torch.full_like(xd, float("nan"))  # (queued on the default stream before the calls)
     a.process_device_steps(xd.data_ptr(), B, C * B, ya.data_ptr(), B, C * B, B, K, 0)
-    a.synchronize()
+    got = ya.cpu().numpy()  # the default stream, no synchronisation with the handle
+    yb = torch.empty_like(xd)
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
     b.process_device_steps(xd.data_ptr(), B, C * B, yb.data_ptr(), B, C * B, B, K, s.cuda_stream)
     s.synchronize()
-    assert np.array_equal(ya.cpu().numpy(), yb.cpu().numpy())
+    assert np.isfinite(got).all()
+    assert np.array_equal(got, yb.cpu().numpy())
+    # a second batch of calls on the null stream after a host update (the
+    # handle's own stream) is ordered behind it
+    a.update(hs[::-1].copy())
+    ya2 = torch.full_like(xd, float("nan"))
+    a.process_device_steps(xd.data_ptr(), B, C * B, ya2.data_ptr(), B, C * B, B, K, 0)
+    got2 = ya2.cpu().numpy()
+    assert np.isfinite(got2).all()
+    for c in (0, 7, 15):
+        ref = oracle_mod.FFTConvolver.init(hs[c], B, L)
+        yr = np.concatenate([ref.process(x[k, c]) for k in range(K)])
+        assert_close(got[:, c].reshape(-1), yr, what=f"channel {c}")
+        ref.update(hs[::-1][c].copy())
+        yr2 = np.concatenate([ref.process(x[k, c]) for k in range(K)])
+        assert_close(got2[:, c].reshape(-1), yr2, what=f"channel {c} after update")
 
 
 @pytest.mark.parametrize("B,L", [(256, 40 * 256 + 5), (512, 44 * 512)])

@@ -127,14 +127,20 @@ def test_per_block_tail0_path(amd, oracle_mod):
     assert_close(got, exp, what="per-block tail0")
 
 
-T0FUSED = 512  # VARIANT_T0FUSED: one fused flush kernel instead of five (read per launch)
+T0FUSED = 512  # VARIANT_T0FUSED: the five-kernel flush instead of the fused one (read per launch)
 
 
-def test_fused_flush_bitwise_equals_split(amd, oracle_mod):
-    """The five-kernel end-of-period flush (the default) and the fused one
-    (tail0_fused_kernel, head block 64, VARIANT_T0FUSED) run the same arithmetic in the same order:
+@pytest.mark.parametrize("steps", [False, True])
+def test_fused_flush_bitwise_equals_split(amd, oracle_mod, steps):
+    """The fused end-of-period flush (tail0_fused_kernel, head block 64: the
+    default; four blocks' transforms per wave) and the five-kernel one
+    (VARIANT_T0FUSED) run the same arithmetic in the same order:
     bit-identical outputs, through a NaN block's replay on one channel, and
-    both against the oracle."""
+    both against the oracle -- with per-call launches (the flush transforms
+    every pending block) and with process_device_steps (the head's run wrote
+    the pending spectra; the flush transforms none)."""
+    import torch
+
     head, L, C = 64, 12000, 3
     hs = np.stack([ir(np.random.default_rng(20 + c), L) for c in range(C)])
     outs = []
@@ -145,15 +151,35 @@ def test_fused_flush_bitwise_equals_split(amd, oracle_mod):
             T = conv.tail_block_size
             per = T // head
             rng = np.random.default_rng(21)
-            ys = []
+            xs = []
             for j in range(3 * per + 5):
                 x = np.stack([white(rng, head) for _ in range(C)])
                 if j == per + 4:
                     x[1, 9] = np.nan
-                ys.append(conv.process(x))
-            outs.append(np.concatenate(ys, axis=1))
+                xs.append(x)
+            if steps:
+                xd = torch.from_numpy(np.stack(xs)).to("cuda:0")  # [K][C][head]
+                yd = torch.empty_like(xd)
+                conv.process_device_steps(xd.data_ptr(), head, C * head, yd.data_ptr(), head, C * head, head,
+                                          len(xs), 0)
+                outs.append(np.concatenate(list(yd.cpu().numpy()), axis=1))
+            else:
+                outs.append(np.concatenate([conv.process(x) for x in xs], axis=1))
         finally:
             amd.set_kernel_variant(-1)
+    if not np.array_equal(outs[0], outs[1], equal_nan=True):  # (diagnostics: which one left the oracle)
+        rng = np.random.default_rng(21)
+        refs = [oracle_mod.TwoStageFFTConvolver.init(hs[c], head, L) for c in range(C)]
+        for j in range(3 * per + 5):
+            x = np.stack([white(rng, head) for _ in range(C)])
+            if j == per + 4:
+                x[1, 9] = np.nan
+            for c in range(C):
+                e = refs[c].process(x[c])
+                a0, a1 = outs[0][c, j * head:(j + 1) * head], outs[1][c, j * head:(j + 1) * head]
+                if not np.array_equal(a0, a1, equal_nan=True):
+                    print(f"call {j} ch {c}: fused err {np.nanmax(np.abs(a0 - e)):.3g}, "
+                          f"five err {np.nanmax(np.abs(a1 - e)):.3g}")
     assert np.array_equal(outs[0], outs[1], equal_nan=True)
     rng = np.random.default_rng(21)
     refs = [oracle_mod.TwoStageFFTConvolver.init(hs[c], head, L) for c in range(C)]
