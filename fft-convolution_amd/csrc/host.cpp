@@ -88,6 +88,17 @@ struct DevPtr {
             return fail(e == hipErrorOutOfMemory ? FFTCONV_E_NOMEM : FFTCONV_E_DEVICE,
                         std::string("hipMalloc: ") + hipGetErrorString(e));
         }
+        // (tests: FFTCONV_POISON_ALLOC=1 fills every new device buffer with NaN
+        // bytes, so a read of memory the path never wrote shows in the output
+        // instead of reading whatever the allocator recycled)
+        static const bool poison = [] {
+            const char *v = getenv("FFTCONV_POISON_ALLOC");
+            return v && atoi(v) > 0;
+        }();
+        if (poison) {  // (done before any stream uses the buffer: null stream, then wait)
+            if (hipMemset(p, 0xff, count * sizeof(T)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+                return fail(FFTCONV_E_DEVICE, "poison memset");
+        }
         return FFTCONV_OK;
     }
     size_t bytes() const { return n * sizeof(T); }
@@ -360,10 +371,10 @@ struct UniformCore {
             // (tests: FFTCONV_LA_POISON=1 fills the windows with NaN at init, so a
             // window row read before any anchor wrote it shows in the output)
             if (const char *e = getenv("FFTCONV_LA_POISON"); e && atoi(e) > 0)
-                HIP_TRY(hipMemset(laW.p, 0xff, laW.bytes()));
+                HIP_TRY(hipMemsetAsync(laW.p, 0xff, laW.bytes(), stream));
             if (const char *e = getenv("FFTCONV_LA_PROBE"); e && atoi(e) > 0) {
                 if (int r = la_probe.alloc(1)) return r;
-                HIP_TRY(hipMemset(la_probe.p, 0, sizeof(int)));
+                HIP_TRY(hipMemsetAsync(la_probe.p, 0, sizeof(int), stream));
             }
         }
         // launch timelines (tuning only): FFTCONV_LA_TRACE for the lookahead
@@ -374,7 +385,7 @@ struct UniformCore {
             trace_grid = la_W ? (size_t)la_trace_grid(log2b, (int)S, (int)C) : C;
             if (trace_slots) {
                 if (int r = trace.alloc(trace_slots * trace_grid * 8)) return r;
-                HIP_TRY(hipMemset(trace.p, 0, trace.bytes()));
+                HIP_TRY(hipMemsetAsync(trace.p, 0, trace.bytes(), stream));
                 trace_meta.assign(2 * trace_slots, -1);
             }
         }
@@ -393,7 +404,7 @@ struct UniformCore {
     // per (device, geometry); W_N^k is the handle's own `tw`
     int alloc_large() {
         if (int r = lg_prog.alloc(C)) return r;
-        if (C) HIP_TRY(hipMemset(lg_prog.p, 0, lg_prog.bytes()));
+        if (C) HIP_TRY(hipMemsetAsync(lg_prog.p, 0, lg_prog.bytes(), stream));
         if (int r = lg_v.alloc(C * B)) return r;
         if (int r = lg_tables(device, log2b, &lgt)) return r;
         lgt.twN = tw.p;
@@ -664,6 +675,7 @@ struct UniformCore {
             a.job[0] = job(din, is, dout, os, n);
             a.tw = tw.p;
             a.njobs = 1;
+            a.run_lds_rows = run_lds_rows(log2b, (int)S);
             RunSteps r{(long long)in_step, (long long)out_step, (int)steps};
             HIP_TRY(launch_process_run(log2b, a, r, (int)C, s));
             return FFTCONV_OK;
@@ -720,7 +732,7 @@ struct UniformCore {
             trace_slots = o.trace_slots;
             trace_grid = o.trace_grid;
             if (int r = trace.alloc(trace_slots * trace_grid * 8)) return r;
-            HIP_TRY(hipMemset(trace.p, 0, trace.bytes()));
+            HIP_TRY(hipMemsetAsync(trace.p, 0, trace.bytes(), stream));
             trace_meta.assign(2 * trace_slots, -1);
         }
         if (int r = staging.alloc(o.staging.n)) return r;
@@ -803,6 +815,14 @@ struct TwoStageCore {
     // launches for 456 us at a time, 21.5-22.9 us per cfg3 call, against
     // 7.55 unmasked: profiles/r6/r6b, r6c).  FFTCONV_TAIL_MASKED=1 at creation
     bool tail_masked = false;
+    // the side stream at the device's highest stream priority: HIP maps
+    // streams onto at most GPU_MAX_HW_QUEUES (4) hardware queues, and a side
+    // stream that shared its queue with the head's caller stream serialised
+    // the tail behind the head (the third cfg3 handle of a process ran at
+    // 5.1 us per call against 3.8); high-priority streams get queues of their
+    // own (three handles 3.75 / 3.75 / 3.75 us, profiles/r6/r6m).
+    // FFTCONV_TAIL_PRIO=0 at creation: a normal-priority side stream
+    bool tail_prio = true;
     int run_prio = 0;  // (tuning, FFTCONV_RUN_PRIO at creation: ProcArgs::prio of the runs)
     // tail0 deferred to the end of its period (launch_tail0_flush): the
     // aligned calls' blocks [t0_off, t0_off + t0_n * head_bs) of tail_input
@@ -896,7 +916,13 @@ struct TwoStageCore {
         if (cus > 0 && cus < ncu && !knob)  // (a tuning knob governs every period)
             HIP_TRY(hipStreamCreateWithFlags(&side_open, hipStreamNonBlocking));
         if (cus <= 0 || cus >= ncu) {
-            HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+            if (tail_prio) {
+                int least = 0, greatest = 0;
+                HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+                HIP_TRY(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, greatest));
+            } else {
+                HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+            }
             return FFTCONV_OK;
         }
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
@@ -909,6 +935,7 @@ struct TwoStageCore {
         if (const char *e = getenv("FFTCONV_TS_EXP")) ts_exp = atoi(e);
         if (const char *e = getenv("FFTCONV_TAIL_NARROW")) tail_narrow = atoi(e);
         if (const char *e = getenv("FFTCONV_TAIL_MASKED")) tail_masked = atoi(e) != 0;
+        if (const char *e = getenv("FFTCONV_TAIL_PRIO")) tail_prio = atoi(e) != 0;
         if (const char *e = getenv("FFTCONV_RUN_PRIO")) run_prio = atoi(e);
         if (int r = create_side_stream()) return r;
         // The period events order kernels on this device only (no host wait
@@ -1157,6 +1184,7 @@ struct TwoStageCore {
                     a.job[0].t0m = t0_miss.p;  // (a call that cannot write its spectrum flags the channel)
                 }
                 a.prio = run_prio;
+                a.run_lds_rows = run_lds_rows(head->log2b, (int)head->S);
                 if (head->trace_slots) {  // (FFTCONV_PROC_TRACE: the run's last call, per wave)
                     if (int r = head->trace_fill(a, s)) return r;
                     ++head->la_t;

@@ -417,6 +417,48 @@ __device__ __forceinline__ void mac_rows_range(AccArr &acc, const float2 *Hc, co
     }
 }
 
+// mac_rows_range over a multi-call run's LDS copies of the IR rows (hl) and
+// the FDL ring (xl): the same rows in the same order per slot, so the same
+// bits -- without the HBM / L2 round trip the stream waves otherwise wait on
+// every call (cfg3's head: 62 rows of H and X per call, ~1.6 us)
+template <int LOG2B, class AccArr>
+__device__ __forceinline__ void mac_rows_lds(AccArr &acc, const float2 *hl, const float2 *xl, int curp, int act,
+                                             int t_begin, int t_end, int nw, int sw, int rsub, int f0) {
+    constexpr int B = 1 << LOG2B, F = B / 2;
+    constexpr int RPW = F >= 64 ? 1 : 64 / F, SPL = F >= 64 ? F / 64 : 1;
+    // batches of U rows, every LDS read of a batch issued before its MACs
+    // (one LDS round trip per batch, not per row); rows past t_end read row 0
+    // and are not accumulated
+    constexpr int U = SPL == 1 ? 12 : (SPL == 2 ? 6 : 3);
+    const int STEP = nw * RPW;
+    const float4 *h4 = reinterpret_cast<const float4 *>(hl), *x4 = reinterpret_cast<const float4 *>(xl);
+    int t = t_begin + sw * RPW + rsub;
+    int i = 2 + t;
+    int xi = (curp + i) % act;
+    for (; t < t_end; t += U * STEP) {
+        float4 hv[U][SPL], xv[U][SPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = t + u * STEP < t_end;
+            const int ho = in ? i * F : 0, xo = in ? xi * F : 0;
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) {
+                hv[u][s] = h4[ho + f0 + s * 64];
+                xv[u][s] = x4[xo + f0 + s * 64];
+            }
+            i += STEP;
+            xi += STEP;
+            if (xi >= act) xi -= act;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t + u * STEP < t_end) {
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) acc[s].mac(hv[u][s], xv[u][s]);
+            }
+    }
+}
+
 // launch timeline phase stamp k (0..3) of this wave of a process launch
 // (FFTCONV_PROC_TRACE; job 0 only)
 __device__ __forceinline__ void proc_stamp(const ProcArgs &a, int k) {
@@ -439,6 +481,10 @@ struct RunCarry {
     const float *next_in;   // the next call's input (null: the run's last call)
     float ov[4];            // overlap samples of the chain's lanes (B <= 256)
     int4 st;                // the state word the call stored (hot): the next call's, without a reload
+    // the run's LDS copies of the IR rows and the FDL (ProcArgs::run_lds_rows;
+    // null = the helpers stream the rows from memory): row r at hl / xl + r*B
+    const float2 *hl;
+    float2 *xl;
 };
 
 // Workgroup barrier for LDS data only: this wave's LDS operations complete,
@@ -516,17 +562,20 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
     constexpr bool RH = RUN && Gm::PIPE_EARLY && CNB <= 4;  // (run-carried state: B <= 256)
     float *stage[2] = {ovl, p0l};  // (a run's prefetched input blocks: LDS the step leaves unused)
     const bool hot = RH && rc->hot;
+    // (a run: the spectra of the calls' blocks, double-buffered by stage
+    // parity -- the last helper wave transforms the NEXT call's block while
+    // the chain runs this call's C2R, so a hot call's chain starts at the
+    // conv; then the helper's two transform buffers.  Past the step's LDS:
+    // the run kernel allocates run_lds_bytes)
+    float2 *nxs = reinterpret_cast<float2 *>(smem + Gm::lds_bytes);
+    float2 *nfa = nxs + 2 * B, *nfb = nfa + B;
     // (a run: the state word this step stores when its block succeeds; every
     // thread holds it, so the next call starts without reloading it)
     if constexpr (RH) rc->st = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
     if (wave == 0) {
         // ---- critical chain, one wave: R2C, conv, the C2R error check ----
         if (hot) {
-            // tw, H[0], H[1] and pre in LDS already; the block from the stage
-            const float *sg = stage[rc->par];
-            float *za = reinterpret_cast<float *>(bufA);
-            for (int j = lane; j < B; j += 64) za[j] = sg[j];
-            for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
+            // tw, H[0], H[1], pre and this block's spectrum in LDS already
         } else {
             dma_f32<64>(reinterpret_cast<float *>(bufA), inc, B);   // x[0..B) as packed z[0..B/2)
             for (int m = B / 2 + lane; m < B; m += 64) bufA[m] = make_float2(0.f, 0.f);
@@ -553,22 +602,39 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
         }
         proc_stamp(a, 0);
         if (J.tin) {  // two-stage: append the block to tail_input (:459-461)
-            const float *xb = reinterpret_cast<const float *>(bufA);
+            const float *xb = hot ? stage[rc->par] : reinterpret_cast<const float *>(bufA);
             float *ti = J.tin + c * J.tin_stride;
             for (int j = lane; j < B; j += 64) ti[j] = xb[j];
         }
-        wave_sync();
-        Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
-        Q = Z == bufA ? bufB : bufA;
         float2 *Xcur = Xc + (size_t)cur * B;
         float2 *t0r = J.t0x ? J.t0x + c * J.t0x_stride : nullptr;  // (a run: tail0's copy of the spectrum)
-        for (int m = lane; m < B; m += 64) {
-            const float2 v = real_post<LOG2B, 64>(Z, m, twl);
-            Q[m] = v;
-            Xcur[m] = v;
-            if (t0r) t0r[m] = v;
+        if (hot) {
+            // the spectrum the last helper wave computed during the previous
+            // call (the same transform, bit for bit): to the FDL row, tail0's row
+            Q = nxs + rc->par * B;
+            Z = bufA;
+            float2 *xlc = rc->xl ? rc->xl + (size_t)cur * B : nullptr;  // (the run's LDS ring)
+            for (int m = lane; m < B; m += 64) {
+                const float2 v = Q[m];
+                Xcur[m] = v;
+                if (t0r) t0r[m] = v;
+                if (xlc) xlc[m] = v;
+            }
+        } else {
+            wave_sync();
+            Z = lds_cfft<LOG2B, 64, false, true>(bufA, bufB, twl);  // :229-241
+            Q = Z == bufA ? bufB : bufA;
+            float2 *xlc = nullptr;
+            if constexpr (RH) xlc = rc->xl ? rc->xl + (size_t)cur * B : nullptr;
+            for (int m = lane; m < B; m += 64) {
+                const float2 v = real_post<LOG2B, 64>(Z, m, twl);
+                Q[m] = v;
+                Xcur[m] = v;
+                if (t0r) t0r[m] = v;
+                if (xlc) xlc[m] = v;
+            }
+            wave_sync();
         }
-        wave_sync();
         bool bad = false;  // conv = pre + X (.) H[0] (:256-261), then the C2R error check
         for (int f = lane; f < F; f += 64) {
             const float4 cv = slot_mac(reinterpret_cast<const float4 *>(prel)[f], reinterpret_cast<const float4 *>(Q)[f],
@@ -594,7 +660,12 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
             // waves reduce and store it, and the state, during the C2R below
             const int R = act > 2 ? act - 2 : 0;
             const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
-            if (w0 > 0) mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, R - w0, R, 1, 0, rsub, f0);
+            if (w0 > 0) {
+                bool inl = false;
+                if constexpr (RH) inl = rc->xl != nullptr;
+                if (inl) mac_rows_lds<LOG2B>(acc, rc->hl, rc->xl, curp, act, R - w0, R, 1, 0, rsub, f0);
+                else mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, R - w0, R, 1, 0, rsub, f0);
+            }
 #pragma unroll
             for (int s = 0; s < SPL; ++s) red[s * 64 + lane] = acc[s].get(f0 + s * 64);
             if (lane == 0) s_err = err ? 1 : 0;
@@ -605,9 +676,16 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
         if (RH && wave == 1 && rc->next_in) dma_f32<64>(stage[rc->par ^ 1], rc->next_in + c * J.in_stride, B);
         const int R = act > 2 ? act - 2 : 0;
         const int w0 = R > a.lag ? (R - a.lag) / (NSW + 1) : 0;
-        mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R - w0, NSW, wave - 1, rsub, f0);
+        bool inl = false;
+        if constexpr (RH) inl = rc->xl != nullptr;
+        if (inl) mac_rows_lds<LOG2B>(acc, rc->hl, rc->xl, curp, act, 0, R - w0, NSW, wave - 1, rsub, f0);
+        else mac_rows_range<LOG2B, NTL>(acc, Hc, Xc, J.S, curp, act, 0, R - w0, NSW, wave - 1, rsub, f0);
 #pragma unroll
         for (int s = 0; s < SPL; ++s) red[(wave * SPL + s) * 64 + lane] = acc[s].get(f0 + s * 64);
+        // (the stage DMA has landed before B1: the last wave transforms it after B1)
+        if constexpr (RH) {
+            if (wave == 1 && rc->next_in) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         proc_stamp(a, 2);
     }
     // B1 (B <= 256): every wave at this one barrier -- the chain's share of
@@ -672,6 +750,21 @@ __device__ __forceinline__ bool pipelined_step(const ProcArgs &a, const ProcJob 
                 for (int r = (w == 0 ? 1 : 0); r < RPW; ++r) p = vadd(p, red[w * SPL * 64 + f + r * F]);
             reinterpret_cast<float4 *>(prec)[f] = p;
             if constexpr (RH) reinterpret_cast<float4 *>(prel)[f] = p;  // (the chain's C2R no longer reads prel)
+        }
+        if constexpr (RH) {
+            // the last wave (never in the reduction at B <= 256): the R2C of the
+            // next call's block (:229-241), from the stage wave 1 filled, into
+            // the spectrum buffer of the other parity
+            if (wave == NSW && rc->next_in) {
+                const float *sg = stage[rc->par ^ 1];
+                float *za = reinterpret_cast<float *>(nfa);
+                for (int j = lane; j < B; j += 64) za[j] = sg[j];
+                for (int m = B / 2 + lane; m < B; m += 64) nfa[m] = make_float2(0.f, 0.f);
+                wave_sync();
+                const float2 *Zn = lds_cfft<LOG2B, 64, false, true>(nfa, nfb, twl);
+                float2 *qn = nxs + (rc->par ^ 1) * B;
+                for (int m = lane; m < B; m += 64) qn[m] = real_post<LOG2B, 64>(Zn, m, twl);
+            }
         }
         if (ht == 0) J.state[c] = make_int4(curp, act, 0, la_clear(((flags & ~FLAG_INBUF) ^ FLAG_REV) | FLAG_PRE, a));
         if constexpr (RH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the stage DMA has landed)
@@ -1203,11 +1296,33 @@ __global__ __launch_bounds__(NT, 2) void upols_run_kernel(ProcArgs a, RunSteps r
     // two-stage tail beside the run; 1 = the chain wave, 2 = every wave)
     if (a.prio == 2 || (a.prio == 1 && threadIdx.x < 64)) __builtin_amdgcn_s_setprio(3);
     unsigned t0 = 0;
+    using Gm = Geo<LOG2B, NT>;
+    const int rl = a.run_lds_rows;  // (the IR rows and the FDL in LDS for the run: their row count)
+    if (rl > 0) {
+        float2 *hl = reinterpret_cast<float2 *>(smem + Gm::lds_bytes + 4 * (size_t)Gm::B * sizeof(float2));
+        rc.hl = hl;
+        rc.xl = hl + (size_t)rl * Gm::B;
+        dma_16b<NT>(hl, J.H + c * (size_t)J.S * Gm::B, rl * Gm::B * (int)sizeof(float2));
+    }
     for (int k = 0; k < r.n; ++k) {
         if (a.la_trace && k == r.n - 1) t0 = (unsigned)__builtin_amdgcn_s_memrealtime();  // (the last call's start)
+        if (rl > 0 && !rc.hot) {
+            // the FDL into LDS: at the run's start, and after a call that
+            // did not run the pipelined step to its end (the generic step and
+            // a failed C2R touch only the FDL in memory)
+            dma_16b<NT>(rc.xl, J.X + c * (size_t)J.S * Gm::B, rl * Gm::B * (int)sizeof(float2));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         rc.next_in = k + 1 < r.n ? J.in + r.in_step : nullptr;
-        // (a hot call's state word is the one the previous call stored)
-        const int4 st = rc.hot ? rc.st : J.state[c];
+        // (a hot call's state word is the one the previous call stored; the
+        // reload stays behind the branch -- a speculated load would put a
+        // memory round trip at the start of every call)
+        int4 st = rc.st;
+        if (!rc.hot) {
+            asm volatile("" ::: "memory");
+            st = J.state[c];
+        }
         const bool kept = process_job<LOG2B, NT, false, NTL, true>(a, J, c, st, smem, &rc);
         rc.hot = kept && rc.next_in != nullptr;  // (the next call's block is in stage[par ^ 1])
         rc.par ^= 1;
@@ -1646,9 +1761,13 @@ __global__ __launch_bounds__(64 * ir_nw<LOG2B>()) void ir_segments_wave_kernel(I
         }
     }
     const float *src = a.src + blockIdx.y * a.src_stride;
+    // (a channel's response 8-byte aligned: a point inside the data is one
+    // 8-byte load, half the load instructions of two 4-byte ones)
+    const bool al8 = ((uintptr_t)src & 7) == 0;
     // copy_and_pad (:56-60) of segment i as packed points z[m] = (x[2m], x[2m+1]), m < B/2
     auto point = [&](long long base, int m) {
         const long long i0 = base + 2 * m, i1 = i0 + 1;
+        if (al8 && 2 * m + 1 < B && i1 < a.len_data) return *reinterpret_cast<const float2 *>(src + i0);
         float2 z;
         z.x = (2 * m < B && i0 < a.len_data) ? src[i0] : 0.f;
         z.y = (2 * m + 1 < B && i1 < a.len_data) ? src[i1] : 0.f;
@@ -2359,8 +2478,12 @@ bool gw_supported(int log2b, int S) { return log2b >= 10 && log2b <= kMaxLog2Blo
 // tail then waited for the few CUs the run left free (227 us per period
 // beside the run vs 44 us alone, profiles/r5/r5ai).  The MAC keeps each
 // slot's row order and the transforms the same butterflies: same bits.
+// (at most 256 registers: 2 waves per SIMD -- with a run workgroup's ~240 on
+// the same SIMD; unbounded it took 255 VGPRs + 30 AGPRs, and beside the
+// run's LDS-resident rows (237 VGPRs) it no longer fit: 200 us per tail
+// step instead of 58, profiles/r6/r6h)
 template <int LOG2B, bool ZZ, bool NTL>
-__global__ __launch_bounds__(256, 1) void upols_narrow_kernel(ProcArgs a) {
+__global__ __launch_bounds__(256, 2) void upols_narrow_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const size_t c = blockIdx.x;
     const ProcJob &J = a.job[blockIdx.y];
@@ -2426,16 +2549,33 @@ static hipError_t launch_run_t(const ProcArgs &a, const RunSteps &r, int channel
         args.pipe = (var & VARIANT_NOPIPE) ? 0 : 1;
         args.lag = pipeline_lag(LOG2B);
         auto kern = (var & VARIANT_NT) ? upols_run_kernel<LOG2B, PNT, true> : upols_run_kernel<LOG2B, PNT, false>;
-        if (Gm::lds_bytes > 64 * 1024) {
+        // (+ the run-carried spectra and the next block's transform buffers,
+        // pipelined_step; + the IR rows and the FDL when they fit)
+        const size_t lds = Gm::lds_bytes + 4 * (size_t)Gm::B * sizeof(float2) +
+                           (size_t)a.run_lds_rows * 2 * Gm::B * sizeof(float2);
+        if (a.run_lds_rows < 0 || lds > 160 * 1024) return hipErrorInvalidValue;
+        if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)Gm::lds_bytes);
+                                               (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(kern, dim3(channels), dim3(PNT), Gm::lds_bytes, s, args, r);
+        hipLaunchKernelGGL(kern, dim3(channels), dim3(PNT), lds, s, args, r);
         return hipGetLastError();
     } else {
         return hipErrorNotSupported;
     }
+}
+// the row count of a run's LDS-resident IR rows + FDL (ProcArgs::run_lds_rows):
+// S when a run workgroup's LDS stays within 96 KiB -- room left for a 64 KiB
+// two-stage tail workgroup on the same CU (cfg3: B 64, S 64 -> 74 KiB) -- and
+// only for the run-carried pipelined step (B <= 256); else 0
+int run_lds_rows(int log2b, int S) {
+    if (log2b < 6 || log2b > 8 || S < 2) return 0;
+    if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NORUNLDS)) return 0;
+    const size_t B = (size_t)1 << log2b;
+    const size_t base = (log2b == 6 ? Geo<6, 256>::lds_bytes : (log2b == 7 ? Geo<7, 256>::lds_bytes : Geo<8, 256>::lds_bytes)) +
+                        4 * B * sizeof(float2);
+    return base + (size_t)S * 2 * B * sizeof(float2) <= 96 * 1024 ? S : 0;
 }
 bool run_supported(int log2b) {
     if (g_variant != VARIANT_AUTO && (g_variant & VARIANT_NORUN)) return false;

@@ -67,6 +67,7 @@ enum : int {
     VARIANT_T0FUSED = 512,  // deferred tail0 at B = 64: the five-kernel flush instead of the fused one (bit-identical)
     VARIANT_NOGW = 1024,    // B >= 1024: no far-row windows, every step sums its far rows itself (tests)
     VARIANT_NORUN = 2048,   // process_device_steps: one launch per call (else a run of a period's calls per launch)
+    VARIANT_NORUNLDS = 4096,  // runs stream the FDL / IR rows from memory (else from LDS copies when they fit; same bits)
     VARIANT_AUTO = 0x7fffffff
 };
 void set_variant(int v);
@@ -202,6 +203,10 @@ struct ProcArgs {
     // multi-call run (upols_run_kernel): the waves' issue priority (s_setprio;
     // 0 = the default) -- the latency-bound chain beside the two-stage tail
     int prio;
+    // multi-call run: the FDL rows and IR rows held in LDS for the whole run
+    // (the pipelined step's helpers stream them from LDS), when they fit: the
+    // row count S of the job, 0 = off (the rows stream from HBM / L2)
+    int run_lds_rows;
 };
 
 struct IrArgs {
@@ -258,6 +263,7 @@ struct RunSteps {
     int n;
 };
 bool run_supported(int log2b);
+int run_lds_rows(int log2b, int S);  // a run's LDS-resident rows for this geometry (0 = none)
 hipError_t launch_process_run(int log2b, const ProcArgs &a, const RunSteps &r, int channels, hipStream_t s);
 hipError_t launch_ir_segments(int log2b, const IrArgs &a, int channels, hipStream_t s);
 hipError_t launch_twostage_accum(const TwoStageAccumArgs &a, int channels, hipStream_t s);

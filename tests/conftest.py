@@ -24,6 +24,26 @@ def oracle_mod():
     return oracle
 
 
+def _reset_torch_stream():
+    if "torch" in sys.modules:
+        torch = sys.modules["torch"]
+        if torch.cuda.is_available():
+            torch.cuda.set_stream(torch.cuda.default_stream())
+
+
+@pytest.fixture(autouse=True)
+def _torch_default_stream(request):
+    """Every gpu test starts and ends on torch's default stream: a test that
+    leaves another current stream (torch.cuda.set_stream) would make a later
+    test's torch copies and stream-0 library calls run on different streams."""
+    gpu = request.node.get_closest_marker("gpu") is not None
+    if gpu:
+        _reset_torch_stream()
+    yield
+    if gpu:
+        _reset_torch_stream()
+
+
 @pytest.fixture(scope="session")
 def amd():
     import fftconv_amd

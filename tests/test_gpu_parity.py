@@ -643,7 +643,7 @@ def test_cfg2_full_size_sampled_channels(amd, oracle_mod):
     xd = torch.from_numpy(x).to(dev)
     yd = torch.empty_like(xd)
     s = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(s)
+    s.wait_stream(torch.cuda.current_stream(dev))
     stream = s.cuda_stream
     assert stream != 0
     for s in range(steps):
