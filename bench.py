@@ -25,6 +25,13 @@ default) ahead of that run's process_device_steps call, not one per block
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused
 kernel and `cpu_baseline` from the oracle port on this host (rank 0, N=1).
+`roofline.launch_us` is the kernel's average duration from a rocprofv3
+--kernel-trace --stats child pass of this same command (run before this
+process touches the GPU; `--kt-out DIR` keeps its csv files, profiles/r6/
+holds the committed ones), so `frac` = bytes_per_launch / launch_us / 8 TB/s
+is reproducible from that summary; the HIP-event time of the timed steps is
+`launch_us_events`.  `traffic` comes from two more child passes (--pmc
+FETCH_SIZE, then WRITE_SIZE).
 """
 from __future__ import annotations
 

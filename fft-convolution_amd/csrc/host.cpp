@@ -304,6 +304,9 @@ struct UniformCore {
     // steps so far (the anchor class of the next one)
     bool gw_ok = false;
     bool narrow = false;  // 2048 <= B <= 8192: 256-thread step workgroups (ProcArgs::narrow)
+    // (a two-stage tail's one-block step: arrive on this signal, ProcArgs::sig; null = none)
+    unsigned *sig_arrive = nullptr;
+    unsigned sig_arrive_val = 0;
     int gw_p = 0;
     DevPtr<float2> gwin;
     unsigned long long gw_t = 0;
@@ -643,6 +646,11 @@ struct UniformCore {
         lg_fill(a, n);
         a.narrow = narrow ? 1 : 0;
         a.gw_p = gw_p;  // (every launch: the split order)
+        if (sig_arrive && n == B && !large) {
+            a.sig = sig_arrive;
+            a.sig_val = sig_arrive_val;
+            a.sig_mode = 1;
+        }
         if (gw_p && n == B && gw_windows_allowed()) {
             // a one-block step reads the live windows, then the channels of
             // class gw_t mod P anchor theirs for their next P blocks
@@ -650,6 +658,7 @@ struct UniformCore {
             a.gw_t = (int)(gw_t % (unsigned long long)gw_p);
             HIP_TRY(launch_process(log2b, a, (int)C, s));
             if (after_step) HIP_TRY(hipEventRecord(after_step, s));
+            a.sig_mode = 0;  // (the anchor does not arrive)
             HIP_TRY(launch_gw_anchor(log2b, a, (int)C, s));
             ++gw_t;
             return FFTCONV_OK;
@@ -805,6 +814,22 @@ struct TwoStageCore {
     // ev_tail_done: everything of it, its window anchor included (quiesce)
     hipEvent_t ev_main = nullptr, ev_tail = nullptr, ev_tail_done = nullptr;
     bool tail_in_flight = false;
+    // The head of the period after a tail's period reads that tail's output.
+    // Instead of a barrier packet on the head's stream at every period end
+    // (hipStreamWaitEvent: ~7 us of cfg3's ~240 us period, r6p), the next
+    // run waits on the device (ProcArgs::sig): tail step k releases
+    // tsig[1] = k, and `pend` names the tail the next head work must follow
+    // (0 = none); every other path waits on that tail's event ev_tk[k & 1].
+    DevPtr<unsigned> tsig;  // {arrivals, last tail done, wait timeouts, -}
+    hipEvent_t ev_tk[2] = {nullptr, nullptr};
+    bool tk_sig[2] = {false, false};  // tail k arrives on tsig
+    unsigned tseq = 0, pend = 0;
+    // the event wait for a pending tail, on stream s (every path but a run)
+    int resolve_pend(hipStream_t s) {
+        if (pend) HIP_TRY(hipStreamWaitEvent(s, ev_tk[pend & 1], 0));
+        pend = 0;
+        return FFTCONV_OK;
+    }
     int ts_exp = 0;  // (timing probes, FFTCONV_TS_EXP at creation; never in tests)
     // the tail's step on 256-thread workgroups: 0 never, 1 in periods that ran
     // as multi-call runs, 2 always (FFTCONV_TAIL_NARROW at creation)
@@ -840,11 +865,27 @@ struct TwoStageCore {
     // [C]: a run's call of this channel wrote no spectrum to t0_xs (its head
     // buffer out of step with tail_input); the flush recomputes and clears it
     DevPtr<int> t0_miss;
+    DevPtr<int> t0_trace;  // (tuning, FFTCONV_T0_TRACE: the fused flush's phase stamps, [C][8], last flush)
     Scratch scratch;
     mutable StreamOrder order;
 
     ~TwoStageCore() {
         DeviceGuard g(device);
+        if (t0_trace.n) {  // (FFTCONV_T0_TRACE: per-phase medians of the last flush, us)
+            (void)hipDeviceSynchronize();
+            std::vector<int> h(t0_trace.n);
+            if (hipMemcpy(h.data(), t0_trace.p, t0_trace.bytes(), hipMemcpyDeviceToHost) == hipSuccess) {
+                std::vector<double> ph[5];
+                for (size_t c = 0; c < C; ++c)
+                    for (int k = 0; k < 5; ++k) ph[k].push_back((double)(unsigned)(h[c * 8 + k + 1] - h[c * 8]) / 100.0);
+                fprintf(stderr, "t0 flush phases (us from the workgroup's start, median over channels):");
+                for (auto &v : ph) {
+                    std::sort(v.begin(), v.end());
+                    fprintf(stderr, " %.2f", v[v.size() / 2]);
+                }
+                fprintf(stderr, "\n");
+            }
+        }
         if (side) { (void)hipStreamSynchronize(side); (void)hipStreamDestroy(side); }
         if (side_open) { (void)hipStreamSynchronize(side_open); (void)hipStreamDestroy(side_open); }
         if (stream) (void)order.drain(stream);
@@ -852,6 +893,8 @@ struct TwoStageCore {
         if (stream) (void)hipStreamDestroy(stream);
         if (ev_main) (void)hipEventDestroy(ev_main);
         if (ev_tail) (void)hipEventDestroy(ev_tail);
+        for (auto &e : ev_tk)
+            if (e) (void)hipEventDestroy(e);
         if (ev_tail_done) (void)hipEventDestroy(ev_tail_done);
     }
 
@@ -863,6 +906,11 @@ struct TwoStageCore {
         if (int r = order.enter(stream)) return r;
         if (tail_in_flight) HIP_TRY(hipStreamWaitEvent(stream, ev_tail_done, 0));
         HIP_TRY(hipStreamSynchronize(stream));
+        if (tsig.n) {  // (a run that gave up waiting for its tail: never expected)
+            unsigned to = 0;
+            HIP_TRY(hipMemcpy(&to, tsig.p + 2, sizeof(unsigned), hipMemcpyDeviceToHost));
+            if (to) return fail(FFTCONV_E_DEVICE, "a two-stage run timed out waiting for its tail step");
+        }
         return FFTCONV_OK;
     }
 
@@ -946,6 +994,10 @@ struct TwoStageCore {
         const unsigned evf = hipEventDisableTiming | ((ts_exp & 4) ? 0u : hipEventDisableSystemFence);
         HIP_TRY(hipEventCreateWithFlags(&ev_main, evf));
         HIP_TRY(hipEventCreateWithFlags(&ev_tail, evf));
+        for (auto &e : ev_tk) HIP_TRY(hipEventCreateWithFlags(&e, evf));
+        if (int r = tsig.alloc(4)) return r;
+        HIP_TRY(hipMemsetAsync(tsig.p, 0, tsig.bytes(), stream));
+        tseq = pend = 0;
         HIP_TRY(hipEventCreateWithFlags(&ev_tail_done, evf));
         for (auto *b : {&out0, &pre0, &out1, &pre1, &tin_buf[0], &tin_buf[1]}) {
             if (int r = b->alloc(C * T)) return r;
@@ -965,6 +1017,8 @@ struct TwoStageCore {
             if (int r = t0_ov.alloc(C * head_bs)) return r;
             if (int r = t0_cv.alloc(C * t0_nmax * head_bs)) return r;
             if (int r = t0_miss.alloc(C)) return r;
+            if (getenv("FFTCONV_T0_TRACE"))
+                if (int r = t0_trace.alloc(C * 16)) return r;  // (C x 4 int4: the replay's proc_stamp too)
             HIP_TRY(hipMemsetAsync(t0_err.p, 0, t0_err.bytes(), stream));
             if (t0_miss.n) HIP_TRY(hipMemsetAsync(t0_miss.p, 0, t0_miss.bytes(), stream));
         }
@@ -973,7 +1027,7 @@ struct TwoStageCore {
     }
 
     // tail_convolver0.process (:464-472) of the deferred blocks, in one pass
-    int flush_t0(hipStream_t s) const {
+    int flush_t0(hipStream_t s, hipEvent_t done = nullptr) const {
         if (t0_n == 0) return FFTCONV_OK;
         Tail0Args a{};
         a.pa.job[0] = tail0->job(tail_input() + t0_off, T, tail_output0 + t0_off, T, head_bs);
@@ -984,7 +1038,8 @@ struct TwoStageCore {
         a.n = (int)t0_n; a.nmax = (int)t0_nmax;
         a.k0 = (int)std::min(t0_have, t0_n);
         a.miss = t0_miss.p;
-        HIP_TRY(launch_tail0_flush(tail0->log2b, a, (int)C, s));
+        if (t0_trace.n) a.pa.la_trace = reinterpret_cast<int4 *>(t0_trace.p);  // (FFTCONV_T0_TRACE)
+        HIP_TRY(launch_tail0_flush(tail0->log2b, a, (int)C, s, done));
         t0_n = t0_have = 0;  // (only once the flush is enqueued: a failed launch keeps the blocks pending)
         return FFTCONV_OK;
     }
@@ -1053,16 +1108,22 @@ struct TwoStageCore {
     // (Starting the tail before the flush, beside it, was slower: 8.17 vs
     // 7.62 us per cfg3 step, profiles/r4/r4u_ab_cfg3_tail_early_rejected.log.)
     int end_of_period(hipStream_t s) {
-        if (int r = flush_t0(s)) return r;  // (tail_output0 is complete before the swap)
+        // ev_main (the tail may start) recorded by the flush kernel's own
+        // completion (hipExtLaunchKernel) instead of a marker packet after it
+        // (cfg3 A/B 3.669 -> 3.645 us per call, r6p); FFTCONV_TS_EXP bit 4: the marker
+        const bool ev_on_flush = !(ts_exp & 16) && t0_n > 0 && tail && !(ts_exp & 8);
+        if (int r = flush_t0(s, ev_on_flush ? ev_main : nullptr)) return r;  // (tail_output0 is complete before the swap)
         std::swap(tail_precalculated0, tail_output0);                         // :473-475
         std::swap(tail_precalculated, tail_output);                           // :483
         // work after this point reads the swapped-in tail_precalculated: it is
-        // the previous period's tail result, so wait for that kernel here
+        // the previous period's tail result, which the next head work waits
+        // for (`pend`: a run on the device, every other path on its event)
         // (FFTCONV_TS_EXP bit 0, timing probes only: no wait -- racy)
-        if (tail_in_flight && !(ts_exp & 1)) HIP_TRY(hipStreamWaitEvent(s, ev_tail, 0));
-        if (tail) {                                                            // :484-485
+        if (int r = resolve_pend(s)) return r;  // (a period of one call: the previous one's)
+        if (tail_in_flight && !(ts_exp & 1)) pend = tseq;
+        if (tail && !(ts_exp & 8)) {  // :484-485 (FFTCONV_TS_EXP bit 3, timing probes only: no tail at all)
             hipStream_t ts = period_runs && side_open ? side_open : side;
-            HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
+            if (!ev_on_flush) HIP_TRY(hipEventRecord(ev_main, s));  // this period's tail_input is complete
             HIP_TRY(hipStreamWaitEvent(ts, ev_main, 0));
             // ev_main follows the previous tail's step only (ev_tail): its
             // window anchor ran on its own side stream, so a tail on the other
@@ -1072,8 +1133,15 @@ struct TwoStageCore {
             // window anchor: 19 us of cross-queue wait behind the anchor, r5p;
             // starting the tail before the flush gained nothing, r5s)
             tail->narrow = (tail_narrow == 2 || (tail_narrow == 1 && period_runs)) && !tail->large;
-            if (int r = tail->process_device(tail_input(), T, tail_output, T, T, ts, 0, nullptr, nullptr, ev_tail))
-                return r;
+            const unsigned seq = tseq + 1 == 0 ? 1 : tseq + 1;  // (0 = none)
+            const bool use_sig = !tail->large && !(ts_exp & 32);  // (FFTCONV_TS_EXP bit 5: events only)
+            tail->sig_arrive = use_sig ? tsig.p : nullptr;
+            tail->sig_arrive_val = seq;
+            const int rr = tail->process_device(tail_input(), T, tail_output, T, T, ts, 0, nullptr, nullptr, ev_tk[seq & 1]);
+            tail->sig_arrive = nullptr;
+            if (rr) return rr;
+            tk_sig[seq & 1] = use_sig;
+            tseq = seq;
             HIP_TRY(hipEventRecord(ev_tail_done, ts));
             tail_in_flight = true;
             last_ts = ts;
@@ -1089,6 +1157,7 @@ struct TwoStageCore {
     int process_device(const float *din, size_t is, float *dout, size_t os, size_t len, hipStream_t s) {
         if (len > head_bs) return fail(FFTCONV_E_INVALID, "assertion failed: input.len() <= self.head_block_size");
         if (len == 0 || C == 0) return FFTCONV_OK;
+        if (int r = resolve_pend(s)) return r;
         if (len == head_bs && tail_input_fill % head_bs == 0 && tail_input_fill + len <= T &&
             head->log2b <= kMaxLog2Fused) {
             // aligned call: one sub-chunk, and tail0 consumes exactly this block.
@@ -1185,6 +1254,14 @@ struct TwoStageCore {
                 }
                 a.prio = run_prio;
                 a.run_lds_rows = run_lds_rows(head->log2b, (int)head->S);
+                if (pend && tk_sig[pend & 1]) {  // (the run waits for the tail on the device)
+                    a.sig = tsig.p;
+                    a.sig_val = pend;
+                    a.sig_mode = 2;
+                    pend = 0;
+                } else if (int r = resolve_pend(s)) {
+                    return r;
+                }
                 if (head->trace_slots) {  // (FFTCONV_PROC_TRACE: the run's last call, per wave)
                     if (int r = head->trace_fill(a, s)) return r;
                     ++head->la_t;
@@ -1234,6 +1311,7 @@ struct TwoStageCore {
         tail_input_fill = 0;
         precalculated_pos = 0;
         tail_in_flight = false;
+        pend = 0;  // (quiesce waited for every tail)
         t0_n = t0_have = 0;  // (the deferred blocks' state is reset with everything else)
         if (t0_miss.n) HIP_TRY(hipMemsetAsync(t0_miss.p, 0, t0_miss.bytes(), stream));
         HIP_TRY(hipStreamSynchronize(stream));

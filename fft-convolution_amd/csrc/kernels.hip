@@ -23,6 +23,7 @@
 
 #include "fft_lds.hpp"
 #include "kernels.hpp"
+#include <hip/hip_ext.h>
 
 namespace fftconv {
 
@@ -457,6 +458,41 @@ __device__ __forceinline__ void mac_rows_lds(AccArr &acc, const float2 *hl, cons
                 for (int s = 0; s < SPL; ++s) acc[s].mac(hv[u][s], xv[u][s]);
             }
     }
+}
+
+// ProcArgs::sig: a tail step's workgroups arrive when their stores are done
+// (each releases at agent scope, then one relaxed add; the last acquires them
+// all and releases sig[1] = sig_val); a run waits for sig[1] >= sig_val
+// (wrap-safe), acquires, and the workgroup's loads of the tail's output come
+// after.  The wait is bounded (~100 ms, counted in sig[2]): the tail it waits
+// for was enqueued a period earlier on a stream of its own, fits a CU beside
+// a run workgroup, and in practice finished long before.
+__device__ __forceinline__ void sig_arrive(const ProcArgs &a) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned n = gridDim.x * gridDim.y;
+        const unsigned prev = __hip_atomic_fetch_add(a.sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == n - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(a.sig, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.sig + 1, a.sig_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+__device__ __forceinline__ void sig_wait(const ProcArgs &a) {
+    if (threadIdx.x == 0) {
+        const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+        while ((int)(__hip_atomic_load(a.sig + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.sig_val) < 0) {
+            __builtin_amdgcn_s_sleep(8);
+            if ((unsigned)__builtin_amdgcn_s_memrealtime() - t0 > 10000000u) {  // (100 MHz: 100 ms)
+                __hip_atomic_fetch_add(a.sig + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
 }
 
 // launch timeline phase stamp k (0..3) of this wave of a process launch
@@ -1262,6 +1298,7 @@ __global__ __launch_bounds__(NT, NT == 512 ? 2 : 4) void upols_process_kernel(Pr
     unsigned t0 = 0;
     if (a.la_trace) t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
     process_job<LOG2B, NT, ZZ, NTL>(a, J, c, J.state[c], smem);
+    if (a.sig_mode == 1) sig_arrive(a);
     if (a.la_trace && blockIdx.y == 0 && (threadIdx.x >> 6) < 4 && (threadIdx.x & 63) == 0) {
         // launch timeline (FFTCONV_PROC_TRACE, tuning): role 6, as upols_la_kernel's record
         const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
@@ -1295,6 +1332,7 @@ __global__ __launch_bounds__(NT, 2) void upols_run_kernel(ProcArgs a, RunSteps r
     // (issue priority over the waves of other kernels on the same SIMD: the
     // two-stage tail beside the run; 1 = the chain wave, 2 = every wave)
     if (a.prio == 2 || (a.prio == 1 && threadIdx.x < 64)) __builtin_amdgcn_s_setprio(3);
+    if (a.sig_mode == 2) sig_wait(a);  // (the previous tail step's output, which the calls add)
     unsigned t0 = 0;
     using Gm = Geo<LOG2B, NT>;
     const int rl = a.run_lds_rows;  // (the IR rows and the FDL in LDS for the run: their row count)
@@ -2153,8 +2191,10 @@ __global__ __launch_bounds__(256) void tail0_commit_kernel(Tail0Args t) {
 // untouched state by the generic step, so the failing block leaves exactly
 // the reference's state
 template <int LOG2B>
-__global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_replay_kernel(Tail0Args t) {
-    constexpr int B = 1 << LOG2B, NT = proc_nt(LOG2B);
+constexpr int t0_replay_nt();
+template <int LOG2B>
+__global__ __launch_bounds__(LOG2B == 6 ? 512 : proc_nt(LOG2B)) void tail0_replay_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B, NT = LOG2B == 6 ? 512 : proc_nt(LOG2B);  // (t0_replay_nt: the fused flush's)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const ProcJob &J = t.pa.job[0];
     const size_t c = blockIdx.x;
@@ -2185,69 +2225,87 @@ __global__ __launch_bounds__(proc_nt(LOG2B)) void tail0_replay_kernel(Tail0Args 
 }
 
 // The whole flush in ONE launch at B = 64 (cfg3's head; one slot chunk per
-// channel), the default there: per channel workgroup
+// channel), the default there: per channel one 512-thread workgroup
 //   (0) every row by LDS-DMA: tail0's IR rows, the previous period's FDL rows,
 //       the pending spectra the head's run wrote (blocks [0, k0)), the
 //       overlap, and the inputs of the blocks still to transform;
 //   (1) the R2C of blocks [r0, n) (r0 = k0, or 0 if the run missed some of
 //       this channel's spectra) into their LDS X rows;
-//   (2) the MAC of tail0_mac_kernel, conv rows to LDS;
-//   (3) each block's C2R and realfft's error check;
-//   (4) overlap-add, overlap save, the FDL rows and the state -- or, if a
-//       block's conv slot 0 is not finite, the block-by-block replay of
-//       tail0_replay_kernel.
-// The same arithmetic in the same order as the five kernels (bit-identical).
+//   (2) the MAC of tail0_mac_kernel, conv rows to LDS; realfft's C2R error
+//       (a non-finite DC / Nyquist of some block's conv) decided right here;
+//   (3) the FDL rows committed, then each block's C2R;
+//   (4) overlap-add, overlap save and the state -- or, on a C2R error, the
+//       block-by-block replay of tail0_replay_kernel from the untouched state.
+// The same arithmetic in the same order as the five kernels (bit-identical:
+// a block's MAC sums its rows in the same order whatever the blocks per
+// thread, and both replays run the generic step on 512 threads).
 // The B = 64 transforms use 16 of a wave's 64 lanes (16 radix-4 butterflies
 // per stage), so each wave runs FOUR blocks' transforms at once, one per
 // 16-lane group, each in its own LDS buffers: the same butterflies per lane
-// group, a quarter of the passes (the r4 fused kernel ran them one at a time,
-// 16 per wave: 46 us per flush; the five kernels beside the tail's anchor,
-// 81 us per cfg3 period, profiles/r5/r5ai).
+// group.  (r4's fused kernel ran one at a time, 16 per wave: 46 us per
+// flush; 256 threads with four groups per wave: 22.4 us per cfg3 flush --
+// MAC 9.4, C2R 6.0, commit 3.4 -- r6o FFTCONV_T0_TRACE.)
 // LDS: [H rows + zero | X rows (q >= -1) + zero rows] (the C2R outputs reuse
-// the H rows once the MAC is done) | tw | 16 groups x 2 B-point buffers |
+// the H rows once the MAC is done, the second 16 transform buffers the X
+// rows once the FDL is committed) | tw | 16 groups x 2 B-point buffers |
 // conv rows (the inputs to transform before the MAC) | overlap | flag
-constexpr int T0F_G = 16;  // lane groups per workgroup (4 waves x 4): transforms per pass
+constexpr int T0F_NT = 512, T0F_J = 4, T0F_G = 16;  // threads; blocks per MAC thread; transform groups of waves 0-3
+template <int LOG2B>
+constexpr int t0_replay_nt() { return LOG2B == 6 ? T0F_NT : proc_nt(LOG2B); }
 template <int LOG2B>
 __host__ __device__ constexpr size_t tail0_fused_lds(int act, int n) {
     constexpr size_t B = (size_t)1 << LOG2B;
-    return tail0_mac_lds<LOG2B>(act, n) + 2 * B * 8 + T0F_G * 2 * B * 8 + (size_t)n * (B / 2) * 16 + B * 4 + 16;
+    return (size_t)(2 * act + 1 + n + T0F_J) * T0_FC * 16 + 2 * B * 8 + T0F_G * 2 * B * 8 + (size_t)n * (B / 2) * 16 +
+           B * 4 + 16;
 }
 template <int LOG2B>
 __host__ __device__ constexpr bool tail0_fused_fits(int act, int n) {
-    return LOG2B == 6 && act >= 1 && n >= 1 && n <= (256 / T0_FC) * T0_J && n <= act + 1 &&
-           tail0_fused_lds<LOG2B>(act, n) <= 160 * 1024;
+    constexpr size_t B = (size_t)1 << LOG2B;
+    // (the C2R's second 16 transform buffers live in the X rows: 2 x 16 x B float2)
+    return LOG2B == 6 && act >= 1 && n >= 1 && n <= (T0F_NT / T0_FC) * T0F_J && n <= act + 1 &&
+           (size_t)(act + n + T0F_J) * T0_FC * 16 >= T0F_G * 2 * B * 8 && tail0_fused_lds<LOG2B>(act, n) <= 160 * 1024;
 }
 template <int LOG2B>
-__global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
-    constexpr int B = 1 << LOG2B, F = B / 2, FC = T0_FC, J = T0_J, RS = J + 1, NT = 256, GL = 16;
+__global__ __launch_bounds__(T0F_NT) void tail0_fused_kernel(Tail0Args t) {
+    constexpr int B = 1 << LOG2B, F = B / 2, FC = T0_FC, J = T0F_J, RS = J + 1, NT = T0F_NT, GL = 16;
     static_assert(F == FC && B / 4 == GL, "one slot chunk per channel, 16 butterflies per stage (B = 64)");
     constexpr float invN = 1.0f / (float)(2 * B);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const ProcJob &J0 = t.pa.job[0];
     const size_t c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int grp = wave * 4 + (lane >> 4), gl = lane & 15;  // this lane's transform group, its lane in it
+    const int grp = wave * 4 + (lane >> 4), gl = lane & 15;  // this lane's transform group (0..31), its lane in it
     const int4 st = J0.state[c];
     const int cur0 = st.x, act = st.y, n = t.n;
     const size_t rows = (size_t)J0.S * B;
     float4 *Hs = reinterpret_cast<float4 *>(smem);   // [act + 1][FC]
     float4 *Xs = Hs + (size_t)(t.act + 2) * FC;       // Xs[q * FC], q >= -1
-    unsigned char *rest = smem + tail0_mac_lds<LOG2B>(t.act, n);
+    unsigned char *rest = smem + (size_t)(2 * t.act + 1 + n + J) * FC * 16;
     float2 *twl = reinterpret_cast<float2 *>(rest);
-    float2 *gA = twl + 2 * B + (size_t)grp * 2 * B, *gB = gA + B;  // this group's transform buffers
-    float4 *cvs = reinterpret_cast<float4 *>(twl + 2 * B + (size_t)T0F_G * 2 * B);  // [n][F]
+    float2 *wb = twl + 2 * B;
+    // groups 0-15: their buffers after tw; groups 16-31 (the C2R only): the X rows' region
+    float2 *gA = grp < T0F_G ? wb + (size_t)grp * 2 * B : reinterpret_cast<float2 *>(Xs - FC) + (size_t)(grp - T0F_G) * 2 * B;
+    float2 *gB = gA + B;
+    float4 *cvs = reinterpret_cast<float4 *>(wb + (size_t)T0F_G * 2 * B);  // [n][F]
     float *ins = reinterpret_cast<float *>(cvs);       // [n][B] inputs to transform, before the MAC
     float *ovs = reinterpret_cast<float *>(cvs + (size_t)n * F);
     int &s_err = *reinterpret_cast<int *>(ovs + B);
     float *ys = reinterpret_cast<float *>(smem);       // [n][2B], over the H rows after the MAC
     const bool geo = act == t.act;  // (not the geometry the LDS was sized for: replay)
     const int r0 = t.miss[c] ? 0 : min(t.k0, n);      // blocks [r0, n) are transformed here
+    // (FFTCONV_T0_TRACE, tuning: phase stamps of thread 0, s_memrealtime)
+    int *tst = t.pa.la_trace ? reinterpret_cast<int *>(t.pa.la_trace) + c * 8 : nullptr;
+    auto stamp = [&](int k) {
+        if (tst && tid == 0) tst[k] = (int)(unsigned)__builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
 
     // ---- (0) every row by LDS-DMA (no VGPRs, all in flight) ----
     const float4 *H = reinterpret_cast<const float4 *>(J0.H + c * rows);
     const float4 *X = reinterpret_cast<const float4 *>(J0.X + c * rows);
     const float4 *xs = reinterpret_cast<const float4 *>(t.xs + (size_t)c * t.nmax * B);
     const int nq = act - 1 + n;
+    constexpr int NWV = NT / 64;
     if (tid == 0) s_err = geo ? 0 : 1;
     if (geo) {
         for (int idx = tid; idx < FC; idx += NT) Hs[(size_t)act * FC + idx] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2256,13 +2314,13 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
             Xs[(size_t)q * FC + idx % FC] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         const int half = lane >> 5, f = lane & 31;
-        for (int r2 = wave * 2; r2 < act; r2 += 8)  // IR rows, two per wave instruction
+        for (int r2 = wave * 2; r2 < act; r2 += 2 * NWV)  // IR rows, two per wave instruction
             if (r2 + half < act)
                 __builtin_amdgcn_global_load_lds((gptr_t)(H + (size_t)(r2 + half) * F + f),
                                                  (lptr_t)(Hs + (size_t)r2 * FC), 16, 0, 0);
         // X rows q < act - 1 + r0: the previous period's FDL rows, then the
         // spectra of pending blocks [0, r0) (the run's)
-        for (int r2 = wave * 2; r2 < act - 1 + r0; r2 += 8) {
+        for (int r2 = wave * 2; r2 < act - 1 + r0; r2 += 2 * NWV) {
             const int q = r2 + half;
             const float4 *src;
             if (q < act - 1) {
@@ -2277,30 +2335,34 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
         }
         dma_16b<NT>(twl, t.pa.tw, 2 * B * (int)sizeof(float2));
         dma_f32<NT>(ovs, J0.overlap + c * B, B);
-        for (int k = r0 + wave; k < n; k += 4)  // (tail_input blocks: the job's input, stride T)
+        for (int k = r0 + wave; k < n; k += NWV)  // (tail_input blocks: the job's input, stride T)
             dma_f32<64>(ins + (size_t)k * B, J0.in + c * J0.in_stride + (size_t)k * B, B);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    stamp(1);
     if (!geo) goto replay;
     {
-        // ---- (1) R2C of blocks [r0, n) (:229-241) into their X rows, 16 at a time ----
-        for (int k0 = r0; k0 < n; k0 += T0F_G) {
-            const int k = k0 + grp;
-            const bool live = k < n;
-            for (int m = gl; m < B; m += GL)
-                gA[m] = live && m < B / 2 ? make_float2(ins[(size_t)k * B + 2 * m], ins[(size_t)k * B + 2 * m + 1])
-                                          : make_float2(0.f, 0.f);
-            wave_sync();
-            float2 *Z = lds_cfft<LOG2B, GL, false, true>(gA, gB, twl);
-            if (live) {
-                float2 *xr = reinterpret_cast<float2 *>(Xs + (size_t)(k + act - 1) * FC);
-                for (int m = gl; m < B; m += GL) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
+        // ---- (1) R2C of blocks [r0, n) (:229-241) into their X rows, 16 at a time (waves 0-3) ----
+        if (grp < T0F_G) {
+            for (int k0 = r0; k0 < n; k0 += T0F_G) {
+                const int k = k0 + grp;
+                const bool live = k < n;
+                for (int m = gl; m < B; m += GL)
+                    gA[m] = live && m < B / 2 ? make_float2(ins[(size_t)k * B + 2 * m], ins[(size_t)k * B + 2 * m + 1])
+                                              : make_float2(0.f, 0.f);
+                wave_sync();
+                float2 *Z = lds_cfft<LOG2B, GL, false, true>(gA, gB, twl);
+                if (live) {
+                    float2 *xr = reinterpret_cast<float2 *>(Xs + (size_t)(k + act - 1) * FC);
+                    for (int m = gl; m < B; m += GL) xr[m] = real_post<LOG2B, 64>(Z, m, twl);
+                }
+                wave_sync();
             }
-            wave_sync();
         }
         __syncthreads();
-        // ---- (2) the MAC of tail0_mac_kernel, conv rows to LDS ----
+        stamp(2);
+        // ---- (2) the MAC of tail0_mac_kernel (J blocks per thread), conv rows to LDS ----
         const int fl = tid % FC, g = tid / FC, kb0 = g * J;
         if (kb0 < n) {
             auto xq = [&](int q) { return Xs[q * FC + fl]; };
@@ -2335,12 +2397,29 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
             }
         }
         __syncthreads();
-        // ---- (3) each block's C2R, 16 at a time (realfft's error: a non-finite DC / Nyquist) ----
-        for (int k0 = 0; k0 < n; k0 += T0F_G) {
+        stamp(3);
+        // realfft's C2R error (:264-267): a block's conv DC / Nyquist not finite
+        if (tid < n) {
+            const float2 z = reinterpret_cast<const float2 *>(cvs + (size_t)tid * F)[0];
+            if (!(isfinite(z.x) && isfinite(z.y))) s_err = 1;
+        }
+        __syncthreads();
+        if (s_err) goto replay;
+        // ---- (3) the FDL rows (block k at (cur0 - k) % act, the last act blocks stay) ----
+        float2 *Xc = J0.X + c * rows;
+        const int kf = max(0, n - act);
+        for (int idx = tid; idx < (n - kf) * B; idx += NT) {
+            const int k = kf + (idx >> LOG2B), m = idx & (B - 1);
+            int r = (cur0 - k) % act;
+            if (r < 0) r += act;
+            Xc[(size_t)r * B + m] = reinterpret_cast<const float2 *>(Xs + (size_t)(k + act - 1) * FC)[m];
+        }
+        __syncthreads();  // (the X rows are read: groups 16-31 take their region)
+        // ... then each block's C2R, 32 at a time
+        for (int k0 = 0; k0 < n; k0 += 2 * T0F_G) {
             const int k = k0 + grp;
             const bool live = k < n;
             const float2 *Zc = reinterpret_cast<const float2 *>(cvs + (size_t)min(k, n - 1) * F);
-            if (live && gl == 0 && !(isfinite(Zc[0].x) && isfinite(Zc[0].y))) s_err = 1;
             for (int m = gl; m < B; m += GL) gA[m] = real_pre<LOG2B, 64>(Zc, m, twl);
             wave_sync();
             const float *y = reinterpret_cast<const float *>(lds_cfft<LOG2B, GL, true, true>(gA, gB, twl));
@@ -2351,8 +2430,8 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
             wave_sync();
         }
         __syncthreads();
-        if (s_err) goto replay;
-        // ---- (4) overlap-add (:270-274), overlap save (:283-284), FDL rows, state ----
+        stamp(4);
+        // ---- (4) overlap-add (:270-274), overlap save (:283-284), state ----
         float *outc = J0.out + c * J0.out_stride;
         for (int idx = tid; idx < n * B; idx += NT) {
             const int k = idx >> LOG2B, j = idx & (B - 1);
@@ -2362,14 +2441,6 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
         for (int j = tid; j < B; j += NT) J0.overlap[c * B + j] = ys[(size_t)(n - 1) * 2 * B + B + j] * invN;
         if (st.w & FLAG_INBUF)
             for (int j = tid; j < B; j += NT) J0.inbuf[c * B + j] = 0.f;
-        float2 *Xc = J0.X + c * rows;
-        const int kf = max(0, n - act);
-        for (int idx = tid; idx < (n - kf) * B; idx += NT) {
-            const int k = kf + (idx >> LOG2B), m = idx & (B - 1);
-            int r = (cur0 - k) % act;
-            if (r < 0) r += act;
-            Xc[(size_t)r * B + m] = reinterpret_cast<const float2 *>(Xs + (size_t)(k + act - 1) * FC)[m];
-        }
         if (tid == 0) {
             int cur = (cur0 - n) % act;
             if (cur < 0) cur += act;
@@ -2377,11 +2448,14 @@ __global__ __launch_bounds__(256) void tail0_fused_kernel(Tail0Args t) {
             J0.state[c] = make_int4(cur, act, 0, la_clear(flags, t.pa));
             t.miss[c] = 0;
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(5);
         return;
     }
 replay:
     // tail_convolver0.process block by block from the untouched state (the
-    // FDL, the overlap and the state word are not written above)
+    // FDL, the overlap and the state word are not written above), on the
+    // generic step of 512 threads, as tail0_replay_kernel at B = 64
     if (tid == 0) t.miss[c] = 0;
     for (int k = 0; k < n; ++k) {
         ProcJob Jk = J0;
@@ -2488,6 +2562,7 @@ __global__ __launch_bounds__(256, 2) void upols_narrow_kernel(ProcArgs a) {
     const size_t c = blockIdx.x;
     const ProcJob &J = a.job[blockIdx.y];
     process_job<LOG2B, 256, ZZ, NTL>(a, J, c, J.state[c], smem);
+    if (a.sig_mode == 1) sig_arrive(a);
 }
 
 template <int LOG2B>
@@ -2593,7 +2668,7 @@ hipError_t launch_process_run(int log2b, const ProcArgs &a, const RunSteps &r, i
 }
 
 template <int LOG2B>
-static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s) {
+static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s, hipEvent_t done) {
     if constexpr (LOG2B >= 6 && LOG2B <= 9) {
         constexpr int B = 1 << LOG2B, KT = 256 / (B / 2), NT = proc_nt(LOG2B);
         if (a.n <= 0 || a.n > a.nmax) return hipErrorInvalidValue;
@@ -2620,7 +2695,11 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
                                                        (int)fl);
                     e != hipSuccess)
                     return e;
-                hipLaunchKernelGGL(fk, dim3(channels), dim3(256), fl, s, t);
+                if (done) {  // (the event on the kernel's own completion: no marker packet of its own)
+                    hipExtLaunchKernelGGL(fk, dim3(channels), dim3(T0F_NT), fl, s, nullptr, done, 0, t);
+                    return hipGetLastError();
+                }
+                hipLaunchKernelGGL(fk, dim3(channels), dim3(T0F_NT), fl, s, t);
                 return hipGetLastError();
             }
         }
@@ -2632,8 +2711,15 @@ static hipError_t launch_tail0_t(const Tail0Args &a, int channels, hipStream_t s
         hipLaunchKernelGGL(mk, dim3(channels, F / FC), dim3(256), lds, s, t);
         hipLaunchKernelGGL(tail0_c2r_kernel<LOG2B>, dim3(channels, a.n), dim3(64), 4 * B * sizeof(float2), s, t);
         hipLaunchKernelGGL(tail0_commit_kernel<LOG2B>, dim3(channels, (a.n + KT - 1) / KT), dim3(256), 0, s, t);
-        constexpr size_t rep_lds = Geo<LOG2B, NT>::lds_bytes;  // (the generic step)
-        hipLaunchKernelGGL(tail0_replay_kernel<LOG2B>, dim3(channels), dim3(NT), rep_lds, s, t);
+        constexpr int RNT = t0_replay_nt<LOG2B>();
+        static_assert(RNT == (LOG2B == 6 ? 512 : proc_nt(LOG2B)), "tail0_replay_kernel's thread count");
+        constexpr size_t rep_lds = Geo<LOG2B, RNT>::lds_bytes;  // (the generic step)
+        if (done) {
+            hipExtLaunchKernelGGL(tail0_replay_kernel<LOG2B>, dim3(channels), dim3(RNT), (std::uint32_t)rep_lds, s,
+                                  nullptr, done, 0, t);
+            return hipGetLastError();
+        }
+        hipLaunchKernelGGL(tail0_replay_kernel<LOG2B>, dim3(channels), dim3(RNT), rep_lds, s, t);
         return hipGetLastError();
     } else {
         return hipErrorNotSupported;
@@ -2644,13 +2730,13 @@ bool tail0_defer_supported(int log2b, int act, int nmax) {
     const int F = (1 << log2b) / 2, FC = F < T0_FC ? F : T0_FC;
     return nmax <= (256 / FC) * T0_J && tail0_mac_lds<6>(act, nmax) <= 160 * 1024;
 }
-hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s) {
+hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s, hipEvent_t done) {
     if (channels <= 0) return hipSuccess;
     switch (log2b) {
-        case 6: return launch_tail0_t<6>(a, channels, s);
-        case 7: return launch_tail0_t<7>(a, channels, s);
-        case 8: return launch_tail0_t<8>(a, channels, s);
-        case 9: return launch_tail0_t<9>(a, channels, s);
+        case 6: return launch_tail0_t<6>(a, channels, s, done);
+        case 7: return launch_tail0_t<7>(a, channels, s, done);
+        case 8: return launch_tail0_t<8>(a, channels, s, done);
+        case 9: return launch_tail0_t<9>(a, channels, s, done);
         default: return hipErrorNotSupported;
     }
 }

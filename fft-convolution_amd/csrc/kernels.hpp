@@ -207,6 +207,15 @@ struct ProcArgs {
     // (the pipelined step's helpers stream them from LDS), when they fit: the
     // row count S of the job, 0 = off (the rows stream from HBM / L2)
     int run_lds_rows;
+    // device-side ordering of a two-stage period's head after the previous
+    // tail step, without a barrier packet on the head's stream: sig_mode 1
+    // (the tail's step) -- every workgroup arrives on sig[0], the last one
+    // releases sig[1] = sig_val; sig_mode 2 (a run) -- the workgroups start
+    // once sig[1] has reached sig_val (acquire), or after a bounded wait that
+    // counts in sig[2]
+    unsigned *sig;
+    unsigned sig_val;
+    int sig_mode;
 };
 
 struct IrArgs {
@@ -318,7 +327,8 @@ struct Tail0Args {
 };
 bool tail0_defer_supported(int log2b, int act, int nmax);
 bool tail0_defer_allowed();  // VARIANT_T0BLOCK unset
-hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s);
+// done (optional): an event recorded by the flush's last kernel itself (hipExtLaunchKernel)
+hipError_t launch_tail0_flush(int log2b, const Tail0Args &a, int channels, hipStream_t s, hipEvent_t done = nullptr);
 
 // The fused one-workgroup-per-channel kernels hold two B-point complex
 // buffers in LDS: B <= 8192 (128 KiB).  Larger blocks, up to 2^22, take the

@@ -642,9 +642,9 @@ def test_cfg2_full_size_sampled_channels(amd, oracle_mod):
     dev = torch.device("cuda:0")
     xd = torch.from_numpy(x).to(dev)
     yd = torch.empty_like(xd)
-    s = torch.cuda.Stream(dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    stream = s.cuda_stream
+    st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    stream = st.cuda_stream
     assert stream != 0
     for s in range(steps):
         conv.process_device(xd.data_ptr() + 4 * s * B, steps * B, yd.data_ptr() + 4 * s * B, steps * B, B, stream)
@@ -658,6 +658,7 @@ def test_cfg2_full_size_sampled_channels(amd, oracle_mod):
     conv2 = amd.FFTConvolver.init(hs, B, L, channels=C)
     y2d = torch.empty_like(xd)
     x2d = xd * 2.0
+    st.wait_stream(torch.cuda.current_stream(dev))  # (x2d is made on the default stream)
     for s in range(steps):
         conv2.process_device(x2d.data_ptr() + 4 * s * B, steps * B, y2d.data_ptr() + 4 * s * B, steps * B, B, stream)
     torch.cuda.synchronize()
