@@ -286,7 +286,15 @@ struct UniformCore {
     size_t trace_slots = 0, trace_grid = 0;
     std::vector<long long> trace_meta;  // per slot: la_t, grid
     int la_seq = 1;               // launch tag, alternating 1 / 2
-    DevPtr<int> la_probe;         // (tests: FFTCONV_LA_PROBE) post-step state observations
+    DevPtr<int> la_probe;         // (tests: FFTCONV_LA_PROBE) live words the anchors found rewritten
+    // the anchors' copies of the state words [2][C] (ProcJob::sview / vnext):
+    // copy la_seq & 1 is read by the next lookahead launch, the other filled
+    // by its steps.  view_ok: that copy holds the current words -- true only
+    // right after a lookahead launch; every other writer of the state words
+    // (any launch built by job(), update, reset, init, clone) clears it, and
+    // the next lookahead launch copies them first (la_view)
+    DevPtr<int4> lav;
+    mutable bool view_ok = false;
     bool la_all = true;           // next lookahead launch re-anchors every channel
     // long-block path (B > 2^kMaxLog2Fused, large.hip): per-call progress,
     // the inverse's scratch, the geometry's tables; lg_whole: every call
@@ -375,6 +383,8 @@ struct UniformCore {
             // window row read before any anchor wrote it shows in the output)
             if (const char *e = getenv("FFTCONV_LA_POISON"); e && atoi(e) > 0)
                 HIP_TRY(hipMemsetAsync(laW.p, 0xff, laW.bytes(), stream));
+            if (int r = lav.alloc(2 * C)) return r;
+            view_ok = false;
             if (const char *e = getenv("FFTCONV_LA_PROBE"); e && atoi(e) > 0) {
                 if (int r = la_probe.alloc(1)) return r;
                 HIP_TRY(hipMemsetAsync(la_probe.p, 0, sizeof(int), stream));
@@ -428,6 +438,7 @@ struct UniformCore {
         if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), stream));
         std::vector<int4> st(C, make_int4(0, (int)S, 0, 0));
         if (C) HIP_TRY(hipMemcpyAsync(state.p, st.data(), C * sizeof(int4), hipMemcpyHostToDevice, stream));
+        view_ok = false;
         HIP_TRY(hipStreamSynchronize(stream));
         return FFTCONV_OK;
     }
@@ -440,6 +451,7 @@ struct UniformCore {
         a.src = src; a.src_stride = (long long)stride;
         a.len_data = (long long)len_data; a.len_active = (long long)len_active;
         a.tw = tw.p; a.S = (int)S; a.chan0 = (int)chan0; a.update_state = update_state ? 1 : 0;
+        if (update_state) view_ok = false;
         if (large) {
             HIP_TRY(launch_ir_large(log2b, a, lgt, (int)nch, s));
             return FFTCONV_OK;
@@ -540,6 +552,7 @@ struct UniformCore {
         if (inbuf.n) HIP_TRY(hipMemsetAsync(inbuf.p, 0, inbuf.bytes(), s));
         if (pre.n) HIP_TRY(hipMemsetAsync(pre.p, 0, pre.bytes(), s));
         HIP_TRY(launch_reset_state(state.p, (int)C, s));
+        view_ok = false;
         lg_whole = true;
         if (la_W && !la_full_variant()) {  // windows of the zeroed FDL, in the reset
             la_all = false;
@@ -549,7 +562,13 @@ struct UniformCore {
         return FFTCONV_OK;
     }
 
+    // a launch's job: any launch but a lookahead one may write the state
+    // words, so the anchors' copy is stale after it (la_job for those)
     ProcJob job(const float *din, size_t is, float *dout, size_t os, size_t n) const {
+        view_ok = false;
+        return job_raw(din, is, dout, os, n);
+    }
+    ProcJob job_raw(const float *din, size_t is, float *dout, size_t os, size_t n) const {
         ProcJob j{};
         j.H = H.p; j.X = X.p; j.overlap = overlap.p; j.inbuf = inbuf.p; j.pre = pre.p; j.state = state.p;
         j.in = din; j.in_stride = (long long)is; j.out = dout; j.out_stride = (long long)os;
@@ -598,6 +617,19 @@ struct UniformCore {
         la_seq = 3 - la_seq;
         la_all = false;
     }
+    // a lookahead launch's job: the anchors read copy la_seq & 1 of the state
+    // words, the steps fill the other for the next launch (la.hpp
+    // la_anchor_state); after any other writer the words are copied first
+    int la_job(ProcJob &j, const float *din, size_t is, float *dout, size_t os, size_t n, hipStream_t s) {
+        j = job_raw(din, is, dout, os, n);
+        if (!lav.p) return fail(FFTCONV_E_DEVICE, "lookahead launch without the state copies");
+        int4 *rd = lav.p + (size_t)(la_seq & 1) * C, *wr = lav.p + (size_t)((la_seq & 1) ^ 1) * C;
+        if (!view_ok && C) HIP_TRY(hipMemcpyAsync(rd, state.p, C * sizeof(int4), hipMemcpyDeviceToDevice, s));
+        view_ok = true;  // (the launch's steps fill `wr`; la_advance makes it the next read copy)
+        j.sview = rd;
+        j.vnext = wr;
+        return FFTCONV_OK;
+    }
 
     // la_mix / mix / mix_tab: crossfade fusion on the lookahead step (ProcArgs::la_mix);
     // the caller only passes them when this call takes the lookahead launch
@@ -610,7 +642,7 @@ struct UniformCore {
         if (n > (size_t)INT32_MAX) return fail(FFTCONV_E_UNSUPPORTED, "process length exceeds 2^31-1");
         if (n == 0 || C == 0) return FFTCONV_OK;
         ProcArgs a{};
-        a.job[0] = job(din, is, dout, os, n);
+        a.job[0] = job_raw(din, is, dout, os, n);
         a.tw = tw.p;
         a.njobs = 1;
         if (la_ready(n)) {
@@ -623,7 +655,7 @@ struct UniformCore {
             const size_t m = n / B;
             if (m > 1 && la_mix) return fail(FFTCONV_E_INVALID, "crossfade lookahead launch of more than one block");
             for (size_t k = 0; k < m; ++k) {
-                a.job[0] = job(din + k * B, is, dout + k * B, os, B);
+                if (int r = la_job(a.job[0], din + k * B, is, dout + k * B, os, B, s)) return r;
                 a.job[0].mcall = (int)m;
                 a.job[0].mk = (int)k;
                 if (int r = la_fill(a, s)) return r;
@@ -639,6 +671,7 @@ struct UniformCore {
             return FFTCONV_OK;
         }
         if (la_W) la_all = true;  // this launch drops every window
+        view_ok = false;          // (and writes the state words)
         if (trace_slots && !la_W && n == B) {  // (process timelines: one-block calls)
             if (int r = trace_fill(a, s)) return r;
             ++la_t;
@@ -730,6 +763,9 @@ struct UniformCore {
         if (int r = cp(state, o.state)) return r;
         if (int r = cp(laW, o.laW)) return r;
         la_ok = o.la_ok; la_W = o.la_W; la_t = o.la_t; la_seq = o.la_seq; la_all = o.la_all;
+        if (o.lav.n)
+            if (int r = lav.alloc(o.lav.n)) return r;
+        view_ok = false;  // (copied from `state` before the clone's first lookahead launch)
         if (int r = cp(gwin, o.gwin)) return r;
         gw_ok = o.gw_ok; gw_p = o.gw_p; gw_t = o.gw_t;
         large = o.large;
@@ -1480,6 +1516,7 @@ struct CrossfadeCore {
             pair_ok = uniform && pair_supported(a->log2b, (int)a->S);
             HIP_TRY(launch_state_flags(a->state.p, (int)C, FLAG_XSYNC, 0, stream));
             HIP_TRY(launch_state_flags(b->state.p, (int)C, FLAG_XSYNC, 0, stream));
+            a->view_ok = b->view_ok = false;
         }
         stored_len = max_response_length;
         stored_stride = stored_len;
@@ -1653,8 +1690,8 @@ struct CrossfadeCore {
                 // that mixes the two blocks in LDS -- A's and B's clocks
                 // agree (they step together), so one stagger serves both
                 ProcArgs pa{};
-                pa.job[0] = a->job(din, is, dout, os, m);
-                pa.job[1] = b->job(din, is, nullptr, 0, m);
+                if (int r = a->la_job(pa.job[0], din, is, dout, os, m, s)) return r;
+                if (int r = b->la_job(pa.job[1], din, is, nullptr, 0, m, s)) return r;
                 pa.tw = a->tw.p;
                 pa.njobs = 2;
                 if (int r = a->la_fill(pa, s)) return r;

@@ -2913,10 +2913,16 @@ int la_trace_grid(int log2b, int S, int channels) {  // (steady-state launches: 
 // launch would have left them (la_anchor_state, la_rebuild), then the state
 // words pointing at them.  The next process launch is a steady-state launch.
 // ---------------------------------------------------------------------------
+#ifndef FFTCONV_RB_WPC
+#define FFTCONV_RB_WPC 4
+#endif
+#ifndef FFTCONV_RB_UF
+#define FFTCONV_RB_UF LA_UF
+#endif
 template <int LOG2B, bool NTL>
-__global__ __launch_bounds__(LA_NT, 4) void la_rebuild_kernel(ProcArgs a) {
+__global__ __launch_bounds__(LA_NT, FFTCONV_RB_WPC) void la_rebuild_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    la_anchor<LOG2B, NTL>(a, 0, (int)blockIdx.x, smem);
+    la_anchor<LOG2B, NTL, FFTCONV_RB_UF>(a, 0, (int)blockIdx.x, smem);
 }
 
 // the state words of the rebuilt windows (same eligibility test as the

@@ -103,9 +103,22 @@ struct ProcJob {
     int mcall, mk;
     // long-block path (B > 2^kMaxLog2Fused, large.hip): per channel the
     // call's progress {processed, done, C2R failed, arrival counter}, and the
-    // [C][B] scratch between the row and the column passes of the inverse
-    int4 *lg_prog;
-    float2 *lg_v;
+    // [C][B] scratch between the row and the column passes of the inverse.
+    // Lookahead launches (la.hpp, B <= 512: never long-block) use the same
+    // two words for the channels' state words as of the end of the previous
+    // launch, which the anchors read instead of `state` (the step of this
+    // launch rewrites `state` while the anchors run), and the copy the steps
+    // of this launch fill for the next one (null elsewhere).  (Shared words,
+    // not new ones: a larger argument block measurably slows every launch,
+    // +0.2 us per cfg2 step for 32 bytes, r6y.)
+    union {
+        int4 *lg_prog;
+        const int4 *sview;
+    };
+    union {
+        float2 *lg_v;
+        int4 *vnext;
+    };
     // two-stage head of a multi-call launch (upols_run_kernel): its block's
     // spectrum also goes to the deferred tail0's pending-block row
     // t0x + c * t0x_stride (the same R2C tail0_r2c_kernel would compute), so

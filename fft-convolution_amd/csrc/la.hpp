@@ -177,15 +177,18 @@ __device__ __forceinline__ float4 *la_win(const ProcArgs &a, int jb, size_t c, i
 // agree and FLAG_XSYNC says they always have, their FDLs are equal row for
 // row.  B's FDL reads then go to A's copy: A's and B's walkers of a channel run
 // side by side on one XCD (la_kernel_body's XF 3 grid), and the second read
-// of each row is an L2 hit -- one X stream for both windows.  (A state pair
-// seen pre- and post-step simply does not match: B reads its own copy.)
+// of each row is an L2 hit -- one X stream for both windows.  (The anchors
+// read the pair from the launch-start copies, ProcJob::sview.)
 __device__ __forceinline__ bool la_xf_paired(int4 sa, int4 sb) {
     return (sa.w & sb.w & FLAG_XSYNC) && sa.x == sb.x && sa.y == sb.y && sa.z == sb.z &&
            !((sa.w ^ sb.w) & FLAG_INBUF);
 }
 __device__ __forceinline__ const float2 *la_xsrc(const ProcArgs &a, int jb, size_t c) {
     if (jb == 0 || a.la_mix != 3) return a.job[jb].X;
-    const int4 sa = a.job[0].state[c], sb = a.job[1].state[c];
+    // (the anchors' copies of the words: the steps of this launch rewrite `state`)
+    const int4 *va = a.job[0].sview ? a.job[0].sview : a.job[0].state;
+    const int4 *vb = a.job[1].sview ? a.job[1].sview : a.job[1].state;
+    const int4 sa = va[c], sb = vb[c];
     const int4 ua = make_int4(__builtin_amdgcn_readfirstlane(sa.x), __builtin_amdgcn_readfirstlane(sa.y),
                               __builtin_amdgcn_readfirstlane(sa.z), __builtin_amdgcn_readfirstlane(sa.w));
     const int4 ub = make_int4(__builtin_amdgcn_readfirstlane(sb.x), __builtin_amdgcn_readfirstlane(sb.y),
@@ -300,23 +303,18 @@ __device__ __forceinline__ void la_ost(float *p, float v) {
 // the anchor's view of channel c at level lv: its ring position, window and
 // length, or false if this launch opens no window of the level at c.
 //
-// The one shared word of a launch.  The channel's step workgroup stores
-// state[c] once, as ONE 16-byte store from one lane (global_store_dwordx4 of
-// an aligned int4), and an anchor reads it as ONE 16-byte load.  Both are
-// single requests to one 64-byte line: the L2 that holds the line applies
-// the store whole, and a line is written back / filled whole, so a reader on
-// any XCD observes either the pre-step word or the post-step word, never a
-// mix.  (The HIP memory model itself does not promise 16-byte single-copy
-// atomicity; this is the CDNA request / line granularity.)  Typically the
-// pre-step word: the writer's L2 keeps the dirty line until the launch's
-// end-of-kernel release, and the reader's L2 was invalidated at launch start.
-// Either observation is handled exactly: the launch tag (SEQ_MASK) in the
-// word says which one it is, and both branches below rebuild the same ring
-// position and window.  The post-step branch is forced and checked bit for
-// bit by tests/test_gpu_lookahead.py::test_lookahead_post_step_state_word
-// (FFTCONV_LA_PROBE: steps fence their store out, anchors wait and read past
-// L2, and the post-step observations are counted).  Nothing else of the step
-// is read by an anchor (FDL ages >= 1 only, the other window of each level).
+// No word is read while it is written.  A lookahead launch's step rewrites
+// its channels' state words while the launch's anchors run, so the anchors
+// read ProcJob::sview instead: the words as the previous lookahead launch's
+// steps left them (every step stores its final word to ProcJob::vnext as
+// well as to `state`, la_step / la_fallback), or as the host copied them from
+// `state` before a lookahead launch that follows any other state writer
+// (update, reset, a partial or off-path call, clone; UniformCore::la_view).
+// One launch writes the copy and a later one reads it, so the kernel boundary
+// orders them (plain loads and stores, no atomicity assumed).  The copy is
+// the word at the start of this launch: window step 0 serves this launch's
+// step, whose row i meets FDL row (current + i) % act = age i.  The window
+// rebuild runs no steps and reads `state`.
 template <int LOG2B>
 __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c, int lv, int &cur, int &act, int &win,
                                                 int &d) {
@@ -324,39 +322,34 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c
     DBG_CHECK(c >= 0 && c < a.la_channels, 1, c, lv, a.la_channels, 0);  // (site 1: an anchor's channel)
     if (a.la_probe_cnt && !a.la_rebuild) {
         // (tests: FFTCONV_LA_PROBE) let the steps of this launch store their
-        // words (each step fences its store out to memory), then read past
-        // this XCD's L2: the post-step branch below is the one taken
+        // words (each step fences its store out to memory), then read the
+        // live word past this XCD's L2 and count the ones the step already
+        // rewrote: the race the copy keeps the anchors out of
         for (int i = 0; i < 24; ++i) __builtin_amdgcn_s_sleep(127);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (threadIdx.x == 0) {
+            const int lw = __hip_atomic_load(&J.state[c].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (((lw & SEQ_MASK) >> SEQ_SHIFT) == a.la_seq) atomicAdd(a.la_probe_cnt, 1);
+        }
     }
-    const int4 st = J.state[c];
+    const int4 st = (J.sview && !a.la_rebuild) ? J.sview[c] : J.state[c];
     const int sx = __builtin_amdgcn_readfirstlane(st.x), sy = __builtin_amdgcn_readfirstlane(st.y);
     const int sz = __builtin_amdgcn_readfirstlane(st.z), sw = __builtin_amdgcn_readfirstlane(st.w);
     const int pw = la_flag_win(lv);
     act = sy;
     d = la_dnew(c, a, la_per(lv));
+    if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return false;
     if (a.la_rebuild) {
         // window rebuild (no steps in this launch): the window an anchor of
         // the previous launch would have opened, i.e. as after that launch's
         // step -- window step 0 serves the next step (current = sx), whose
         // row i meets FDL row (sx + i) % act = age i - 1 from sx + 1
-        if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return false;
         cur = sx + 1 == act ? 0 : sx + 1;
         win = (sw & pw) ? 0 : 1;
         return true;
     }
-    if (((sw & SEQ_MASK) >> SEQ_SHIFT) == a.la_seq) {
-        // this launch's step has already stored the channel's state: it
-        // opened the window (this channel is scheduled) iff the level is live
-        if (a.la_probe_cnt && threadIdx.x == 0) atomicAdd(a.la_probe_cnt, 1);
-        if (!la_live(sw, lv)) return false;
-        cur = sx + 1 == act ? 0 : sx + 1;
-        win = (sw & pw) ? 1 : 0;
-    } else {
-        if (!la_eligible<LOG2B>(make_int4(sx, sy, sz, sw), J.n)) return false;
-        cur = sx;
-        win = (sw & pw) ? 0 : 1;
-    }
+    cur = sx;
+    win = (sw & pw) ? 0 : 1;
     return true;
 }
 
@@ -365,7 +358,7 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c
 // channel's anchor; the NG row groups (one per wave) combined in group order
 // and stored as one window row per step.
 // ---------------------------------------------------------------------------
-template <int LOG2B, int LV, bool NTL>
+template <int LOG2B, int LV, bool NTL, int UF = LA_UF>
 __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, unsigned char *smem) {
     using LG = LaGeo<LOG2B>;
     constexpr int B = LG::B, P = la_per(LV), FS = LG::FS, NSL = LG::NSL;
@@ -397,8 +390,8 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
     // (plain loads: the nontemporal policy streamed no faster here and cost the
     // step workgroups' cache-resident near rows ~8 % of the launch, r1i_la15_ab)
     if (hi > lo) {
-        if (la_asc(l)) la_walk<LOG2B, true, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
-        else la_walk<LOG2B, false, false, LA_JW, LA_UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        if (la_asc(l)) la_walk<LOG2B, true, false, LA_JW, UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        else la_walk<LOG2B, false, false, LA_JW, UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
     }
     float4 *red = reinterpret_cast<float4 *>(smem);  // [NG-1][JW][FS]
     if (l > 0) {
@@ -905,6 +898,7 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 else if (la_live(flags, lv)) nf |= la_flag_live(lv);
             }
             JC.state[c] = make_int4(curp, act, 0, nf);
+            if (JC.vnext) JC.vnext[c] = make_int4(curp, act, 0, nf);  // (the next launch's anchors)
             if (a.la_probe_cnt) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (tests: the probe)
         }
     } else {
@@ -931,7 +925,10 @@ __device__ __forceinline__ void la_step(const ProcArgs &a, const ProcJob &J, con
                 if (j < JC.mk * B || j >= (JC.mk + 1) * B) o0[j] = 0.f;
         }
         const int done = rest && JC.mk < JC.mcall - 1 ? FLAG_CALLDONE : 0;
-        if (lane == 0) JC.state[c] = make_int4(cur, act, 0, keep | FLAG_INBUF | tag | done);
+        if (lane == 0) {
+            JC.state[c] = make_int4(cur, act, 0, keep | FLAG_INBUF | tag | done);
+            if (JC.vnext) JC.vnext[c] = make_int4(cur, act, 0, keep | FLAG_INBUF | tag | done);
+        }
     }
     if constexpr (XF == 3) la_xf_arrive(a, xcnt, yA, yB, vtab, c);
 }
@@ -947,18 +944,20 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
         if (k) __syncthreads();
         const int c = c0 + k;
         int4 st = J.state[c];
+        bool done = false;
         if (XF == 0 && (st.w & FLAG_CALLDONE)) {
             if (J.mcall > 1 && J.mk > 0) {
                 // done with this multi-block call; its last launch clears the flag
                 if (J.mk == J.mcall - 1 && threadIdx.x == 0) J.state[c] = make_int4(st.x, st.y, st.z, la_clear(st.w & ~FLAG_CALLDONE, a));
-                continue;
+                done = true;
+            } else {
+                // a stale flag: the call that set it stopped before its last
+                // launch (a failed launch).  This is a new call's first
+                // block: process it (the state written below drops the flag)
+                st.w &= ~FLAG_CALLDONE;
             }
-            // a stale flag: the call that set it stopped before its last
-            // launch (a failed launch).  This is a new call's first
-            // block: process it (the state written below drops the flag)
-            st.w &= ~FLAG_CALLDONE;
         }
-        if (XF == 0 && J.mcall > 1 && J.mk == 0 && !la_eligible<LOG2B>(st, J.n)) {
+        if (!done && XF == 0 && J.mcall > 1 && J.mk == 0 && !la_eligible<LOG2B>(st, J.n)) {
             // off the lookahead path at the start of a multi-block call
             // (buffered samples, a short response): the whole call by the
             // reference's chunk loop, here (in / out are the call's at mk 0)
@@ -971,9 +970,10 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
                 s2.w |= FLAG_CALLDONE;
                 J.state[c] = s2;
             }
-            continue;
+            done = true;
         }
-        if (la_eligible<LOG2B>(st, J.n)) {
+        if (done) {
+        } else if (la_eligible<LOG2B>(st, J.n)) {
             const int c1[1] = {c};
             const int4 s1[1] = {st};
             la_step<LOG2B, NTL, 1, XF>(a, J, c1, s1, 1, smem);
@@ -993,6 +993,12 @@ __device__ __attribute__((noinline)) void la_fallback(const ProcArgs *ap, int c0
             for (int j = threadIdx.x; j < J.n; j += LA_NT) o[j] = mix_select(ya[j], yb[j], sel[j]);
         } else {
             process_job<LOG2B, LA_NT, false, NTL>(a, J, (size_t)c, st, smem);
+        }
+        // the channel's final word of this launch, for the next launch's
+        // anchors (same-workgroup global writes are visible after the barrier)
+        if (J.vnext) {
+            __syncthreads();
+            if (threadIdx.x == 0) J.vnext[c] = J.state[c];
         }
     }
 }
@@ -1024,6 +1030,8 @@ __device__ __attribute__((noinline)) void la_fallback_xf(const ProcArgs *ap, int
             Ja.state[c] = ta;
             Jb.state[c] = tb;
         }
+        if (Ja.vnext) Ja.vnext[c] = ta;  // (the next launch's anchors)
+        if (Jb.vnext) Jb.vnext[c] = tb;
     }
     float *t = reinterpret_cast<float *>(smem);
     if (m.approaching) {
@@ -1060,15 +1068,15 @@ __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsign
 // (la_n[2], la_n[1], la_n[0] workgroups) of instance jb; false if ba is past it.
 // The level-3 and level-2 counts are whole XCD rounds (multiples of 8), so
 // every anchor keeps its XCD placement.
-template <int LOG2B, bool NTL>
+template <int LOG2B, bool NTL, int UF = LA_UF>
 __device__ __forceinline__ bool la_anchor(const ProcArgs &a, int jb, int ba, unsigned char *smem) {
     if (ba < a.la_n[2]) {
-        la_anchor_far<LOG2B, 3, NTL>(a, jb, ba, smem);
+        la_anchor_far<LOG2B, 3, NTL, UF>(a, jb, ba, smem);
         return true;
     }
     ba -= a.la_n[2];
     if (ba < a.la_n[1]) {
-        la_anchor_far<LOG2B, 2, NTL>(a, jb, ba, smem);
+        la_anchor_far<LOG2B, 2, NTL, UF>(a, jb, ba, smem);
         // level-1 anchor ba after the level-2 walk: the level-2 workgroups
         // finish first (r4 timeline: 8.9 us median against 13.4 for level 3
         // and ~15 for the in-step level-1 walks they replace)

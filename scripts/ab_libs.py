@@ -45,7 +45,11 @@ for spec in a.libs:
     lib.fftconv_uniform_process_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]
     lib.fftconv_uniform_process_device_steps.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p,
                                                          C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p]
+    envs = {k: v for k, v in knobs[-1].items() if k.startswith("FFTCONV_")}  # read at handle creation
+    os.environ.update(envs)
     h = lib.fftconv_uniform_init_batch(0, Cn, irs.ctypes.data, L, L, B, L)
+    for k in envs:
+        os.environ.pop(k)
     assert h, path
     handles.append((lib, h, torch.empty((16, Cn, B), device="cuda")))
 res = [[] for _ in handles]

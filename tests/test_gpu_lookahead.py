@@ -436,13 +436,14 @@ def test_lookahead_multi_block_calls(amd, oracle_mod, B):
 
 @pytest.mark.parametrize("B,C", [(256, 64), (512, 24)])
 def test_lookahead_post_step_state_word(amd, oracle_mod, monkeypatch, B, C):
-    """The anchors' post-step branch (la.hpp la_anchor_state): an anchor that
-    reads its channel's state word after the same launch's step stored it
-    must rebuild the same ring position and window as one that reads the
-    pre-step word.  FFTCONV_LA_PROBE forces it -- every step fences its word
-    out to memory, every anchor waits and then reads past its L2 -- and counts
-    the post-step observations.  The probed batch must be bit-identical to an
-    unprobed one (which sees the pre-step word) through entry, > 2 level-3
+    """The anchors never read a state word the same launch writes
+    (la.hpp la_anchor_state): they read the launch-start copies
+    (ProcJob::sview) that the previous launch's steps filled or the host
+    refreshed after any other writer.  FFTCONV_LA_PROBE makes the race
+    happen -- every step fences its word out to memory, every anchor waits,
+    reads the LIVE word past its L2 and counts the ones this launch's step has
+    already rewritten -- while the anchors still use the copy.  The probed
+    batch must be bit-identical to an unprobed one through entry, > 2 level-3
     periods, a partial call and its re-entry, a batch update and a NaN block,
     and within tolerance of the oracle."""
     rng = np.random.default_rng(900 + B)
@@ -473,7 +474,7 @@ def test_lookahead_post_step_state_word(amd, oracle_mod, monkeypatch, B, C):
         for c in range(1, C - 1):
             refs[c].process(x[c])
     n = probed.lookahead_probe()
-    print(f"\nB={B} C={C}: {n} post-step state-word observations over {len(chunks)} calls")
-    # every launch opens C/4 + C/16 + C/64 anchors, so the post-step branch
-    # must have run many times (a same-XCD or written-back step word)
-    assert n >= len(chunks), f"only {n} post-step observations"
+    print(f"\nB={B} C={C}: {n} anchors found the live word rewritten over {len(chunks)} calls")
+    # every launch opens C/4 + C/16 + C/64 anchors: the race the copy removes
+    # must have been there many times (a same-XCD or written-back step word)
+    assert n >= len(chunks), f"only {n} rewritten live words"
