@@ -885,6 +885,7 @@ struct TwoStageCore {
     // FFTCONV_TAIL_PRIO=0 at creation: a normal-priority side stream
     bool tail_prio = true;
     int run_prio = 0;  // (tuning, FFTCONV_RUN_PRIO at creation: ProcArgs::prio of the runs)
+    int run_min = 2;   // (tuning, FFTCONV_RUN_MIN at creation: shortest run of calls taken as one launch)
     // tail0 deferred to the end of its period (launch_tail0_flush): the
     // aligned calls' blocks [t0_off, t0_off + t0_n * head_bs) of tail_input
     // still to be convolved by tail_convolver0 (FFTCONV_TAIL0_DEFER=0: off)
@@ -1021,6 +1022,7 @@ struct TwoStageCore {
         if (const char *e = getenv("FFTCONV_TAIL_MASKED")) tail_masked = atoi(e) != 0;
         if (const char *e = getenv("FFTCONV_TAIL_PRIO")) tail_prio = atoi(e) != 0;
         if (const char *e = getenv("FFTCONV_RUN_PRIO")) run_prio = atoi(e);
+        if (const char *e = getenv("FFTCONV_RUN_MIN")) run_min = std::max(1, atoi(e));
         if (int r = create_side_stream()) return r;
         // The period events order kernels on this device only (no host wait
         // reads what they guard), so they carry no system-scope fence: with
@@ -1269,7 +1271,7 @@ struct TwoStageCore {
                                  head->log2b <= kMaxLog2Fused;
             const size_t left = aligned ? (T - tail_input_fill) / head_bs : 0;
             const size_t nrun = std::min(steps - k, left);
-            if (aligned && nrun >= 2 && t0_defer && tail0 && run_supported(head->log2b) &&
+            if (aligned && nrun >= (size_t)run_min && t0_defer && tail0 && run_supported(head->log2b) &&
                 nrun <= (size_t)INT32_MAX && in_step <= (size_t)LLONG_MAX && out_step <= (size_t)LLONG_MAX) {
                 ProcArgs a{};
                 a.job[0] = head->job(din + k * in_step, is, dout + k * out_step, os, len);  // :417

@@ -2,7 +2,8 @@
 """Same-process, interleaved A/B of several builds of libfftconv_amd.so on the
 cfg3 workload (TwoStageFFTConvolver, head 64 / tail 4096, IR 262144, 256
 channels; one process_device_steps call per tail period of 64 head calls).
-Each LIB may carry knobs applied before its timed runs: PATH,variant=1024,lag=8, and
+Each LIB may carry knobs applied before its timed runs: PATH,variant=1024,lag=8,percall=1
+(percall: one process_device_steps call per head call), and
 environment knobs read when its handle is created: PATH,FFTCONV_TAIL_LATE=1.
 usage: ab_cfg3.py LIB1 LIB2 ... [--rounds R] [--periods P]"""
 import argparse
@@ -57,11 +58,17 @@ for spec in a.libs:
             del os.environ[k]
     assert h, path
     handles.append((lib, h, torch.empty((steps, Cn, B), device="cuda"), int(knobs[-1].get("variant", -1)),
-                    int(knobs[-1].get("lag", -1))))
+                    int(knobs[-1].get("lag", -1)), knobs[-1].get("percall", "0") == "1"))
 del irs
 
 
-def period(lib, h, y):
+def period(lib, h, y, percall=False):
+    if percall:  # (one process_device_steps call per head call: the per-call submission)
+        for k in range(steps):
+            r = lib.fftconv_twostage_process_device_steps(h, x[k].data_ptr(), B, Cn * B, y[k].data_ptr(), B, Cn * B,
+                                                           B, 1, s.cuda_stream)
+            assert r == 0, r
+        return
     r = lib.fftconv_twostage_process_device_steps(h, x.data_ptr(), B, Cn * B, y.data_ptr(), B, Cn * B, B, steps,
                                                    s.cuda_stream)
     assert r == 0, r
@@ -70,16 +77,16 @@ def period(lib, h, y):
 res = [[] for _ in handles]
 host = [[] for _ in handles]
 for r in range(a.rounds):
-    for idx, (lib, h, y, var, lag) in enumerate(handles):
+    for idx, (lib, h, y, var, lag, pc) in enumerate(handles):
         lib.fftconv_set_kernel_variant(var)
         if hasattr(lib, "fftconv_set_pipeline_lag"):
             lib.fftconv_set_pipeline_lag(lag)
-        period(lib, h, y)  # warm
+        period(lib, h, y, pc)  # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         t0 = time.perf_counter()
         for _ in range(a.periods):
-            period(lib, h, y)
+            period(lib, h, y, pc)
         t1 = time.perf_counter()
         e1.record(s)
         torch.cuda.synchronize()
