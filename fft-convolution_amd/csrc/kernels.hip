@@ -2800,14 +2800,14 @@ int la_parts(int log2b, int S) {
     if (S < 40) return 0;  // (channels whose active segments drop below D0 + 2 step generically)
     return 1;
 }
-LaDims la_dims(int log2b, int S) {
+LaDims la_dims(int log2b, int S, int jw) {
     LaDims d{};
     d.nlv = la_nlv(S);
     for (int lv = 1; lv <= 3; ++lv) d.per[lv - 1] = la_per(lv);
     const int nsl = log2b >= 7 ? (1 << (log2b - 1)) / 64 : 1;  // LaGeo::NSL
     d.wg[0] = log2b <= LA_MIDIN_MAXLOG ? 0 : 1;                // LaStep::MIDIN: level 1 in the step workgroups
-    d.wg[1] = nsl * (LA_P2 / LA_JW);
-    d.wg[2] = d.nlv == 3 ? nsl * (LA_P3 / LA_JW) : 0;
+    d.wg[1] = nsl * (LA_P2 / jw);
+    d.wg[2] = d.nlv == 3 ? nsl * (LA_P3 / jw) : 0;
     d.pt = LA_PT;
     d.per_all = LA_PER;
     return d;
@@ -2819,8 +2819,9 @@ LaDims la_dims(int log2b, int S) {
 // fold (ProcArgs::la_l1in2): level-1 anchors ride in the level-2 anchor
 // workgroups (one each, after the level-2 walk), so the level-2 count covers
 // the level-1 channels too.
-static void la_counts(ProcArgs &a, int log2b, int S, int C, bool all, bool mid_wg, bool fold = false) {
-    const LaDims d = la_dims(log2b, S);
+static void la_counts(ProcArgs &a, int log2b, int S, int C, bool all, bool mid_wg, bool fold = false,
+                      int jw = LA_JW) {
+    const LaDims d = la_dims(log2b, S, jw);
     int n1 = 0;
     for (int lv = 1; lv <= 3; ++lv) {
         const int P = d.per[lv - 1];
@@ -2919,10 +2920,18 @@ int la_trace_grid(int log2b, int S, int channels) {  // (steady-state launches: 
 #ifndef FFTCONV_RB_UF
 #define FFTCONV_RB_UF LA_UF
 #endif
+// window steps per level-2/3 rebuild workgroup (LA_JW in the process launches):
+// each workgroup walks its rows once for RB_JW steps, so the rows' L2
+// requests scale with P / RB_JW; same rows in the same order per step
+#ifndef FFTCONV_RB_JW
+#define FFTCONV_RB_JW LA_JW
+#endif
+constexpr int RB_JW = FFTCONV_RB_JW;
+static_assert(LA_JW == 8, "la_dims' default window slice (kernels.hpp)");
 template <int LOG2B, bool NTL>
 __global__ __launch_bounds__(LA_NT, FFTCONV_RB_WPC) void la_rebuild_kernel(ProcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    la_anchor<LOG2B, NTL, FFTCONV_RB_UF>(a, 0, (int)blockIdx.x, smem);
+    la_anchor<LOG2B, NTL, FFTCONV_RB_UF, RB_JW>(a, 0, (int)blockIdx.x, smem);
 }
 
 // the state words of the rebuilt windows (same eligibility test as the
@@ -2945,7 +2954,8 @@ static hipError_t launch_rebuild_t(const ProcArgs &a, int channels, hipStream_t 
         return hipErrorNotSupported;
     } else {
         using LG = LaGeo<LOG2B>;
-        constexpr size_t lds = (LG::anchor_bytes + 15) / 16 * 16 + 16;
+        constexpr size_t anchor_bytes = (size_t)(LA_NG - 1) * RB_JW * LG::FS * 16;  // (LaGeo::anchor_bytes at RB_JW)
+        constexpr size_t lds = (anchor_bytes + 15) / 16 * 16 + 16;
         if (!a.laW || a.njobs != 1 || a.job[0].n != (1 << LOG2B)) return hipErrorInvalidValue;
         const double stream = 16.0 * (double)channels * (double)a.job[0].S * (double)(1 << LOG2B);
         const bool ntl = !scan_variant_set() ? stream > 192.0 * 1024 * 1024 : (g_variant & VARIANT_NT) != 0;
@@ -2958,7 +2968,7 @@ static hipError_t launch_rebuild_t(const ProcArgs &a, int channels, hipStream_t 
         args.la_t = a.la_t % LA_PER;
         const int nch = channels - a.la_c0;
         if (nch <= 0) return hipSuccess;
-        la_counts(args, LOG2B, a.job[0].S, channels, true, true);  // (level 1 in workgroups of its own)
+        la_counts(args, LOG2B, a.job[0].S, channels, true, true, false, RB_JW);  // (level 1 in workgroups of its own)
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;

@@ -309,7 +309,7 @@ struct LaDims {
     int pt;           // window rows per channel and window (all levels)
     int per_all;      // the stagger clock's modulus
 };
-LaDims la_dims(int log2b, int S);
+LaDims la_dims(int log2b, int S, int jw = 8);  // (jw: window steps per level-2/3 anchor workgroup, LA_JW)
 // launch timeline records per lookahead launch (FFTCONV_LA_TRACE): the largest grid
 int la_trace_grid(int log2b, int S, int channels);
 hipError_t launch_process_la(int log2b, const ProcArgs &a, int channels, hipStream_t s);

@@ -358,11 +358,12 @@ __device__ __forceinline__ bool la_anchor_state(const ProcArgs &a, int jb, int c
 // channel's anchor; the NG row groups (one per wave) combined in group order
 // and stored as one window row per step.
 // ---------------------------------------------------------------------------
-template <int LOG2B, int LV, bool NTL, int UF = LA_UF>
+template <int LOG2B, int LV, bool NTL, int UF = LA_UF, int JW = LA_JW>
 __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, unsigned char *smem) {
     using LG = LaGeo<LOG2B>;
     constexpr int B = LG::B, P = la_per(LV), FS = LG::FS, NSL = LG::NSL;
-    constexpr int WGA = NSL * (P / LA_JW);
+    constexpr int WGA = NSL * (P / JW);
+    static_assert(P % JW == 0, "window slices");
     const ProcJob &J = a.job[jb];
     // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so the WGA
     // workgroups of one anchor sit 8 apart -- on one XCD, whose L2 then
@@ -374,7 +375,7 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
     int cur, act, win, d;
     if (!la_anchor_state<LOG2B>(a, jb, c, LV, cur, act, win, d)) return;
     const int h = r / NSL;                   // window slice: steps h*JW .. h*JW+JW-1
-    if (h * LA_JW >= d) return;              // (wholly past the window)
+    if (h * JW >= d) return;              // (wholly past the window)
 
     const int tid = threadIdx.x;
     const int l = __builtin_amdgcn_readfirstlane(tid / FS), fl = tid % FS;
@@ -384,29 +385,29 @@ __device__ __forceinline__ void la_anchor_far(const ProcArgs &a, int jb, int b, 
     const size_t rows = (size_t)J.S * B;
     const size_t bytes = rows * sizeof(float2);
     const RowStream hs(J.H + (size_t)c * rows, bytes), xs(la_xsrc(a, jb, (size_t)c) + (size_t)c * rows, bytes);
-    LaAcc acc[LA_JW];
+    LaAcc acc[JW];
 #pragma unroll
-    for (int j = 0; j < LA_JW; ++j) acc[j].zero();
+    for (int j = 0; j < JW; ++j) acc[j].zero();
     // (plain loads: the nontemporal policy streamed no faster here and cost the
     // step workgroups' cache-resident near rows ~8 % of the launch, r1i_la15_ab)
     if (hi > lo) {
-        if (la_asc(l)) la_walk<LOG2B, true, false, LA_JW, UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
-        else la_walk<LOG2B, false, false, LA_JW, UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * LA_JW, cur, act);
+        if (la_asc(l)) la_walk<LOG2B, true, false, JW, UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * JW, cur, act);
+        else la_walk<LOG2B, false, false, JW, UF>(acc, hs, xs, f * 16, f == 0, lo, hi, h * JW, cur, act);
     }
     float4 *red = reinterpret_cast<float4 *>(smem);  // [NG-1][JW][FS]
     if (l > 0) {
 #pragma unroll
-        for (int j = 0; j < LA_JW; ++j) red[((l - 1) * LA_JW + j) * FS + fl] = acc[j].get();
+        for (int j = 0; j < JW; ++j) red[((l - 1) * JW + j) * FS + fl] = acc[j].get();
     }
     __syncthreads();
     if (l == 0) {
 #pragma unroll
-        for (int j = 0; j < LA_JW; ++j) {
-            const int jj = h * LA_JW + j;
+        for (int j = 0; j < JW; ++j) {
+            const int jj = h * JW + j;
             if (jj < d) {
                 float4 p = acc[j].get();
 #pragma unroll
-                for (int q = 1; q < LA_NG; ++q) p = vadd(p, red[((q - 1) * LA_JW + j) * FS + fl]);
+                for (int q = 1; q < LA_NG; ++q) p = vadd(p, red[((q - 1) * JW + j) * FS + fl]);
                 la_wst(la_win(a, jb, c, win, LV, P - d + jj, B) + f, p);
             }
         }
@@ -1068,15 +1069,15 @@ __device__ __attribute__((noinline)) void la_mix_walk(const ProcArgs *ap, unsign
 // (la_n[2], la_n[1], la_n[0] workgroups) of instance jb; false if ba is past it.
 // The level-3 and level-2 counts are whole XCD rounds (multiples of 8), so
 // every anchor keeps its XCD placement.
-template <int LOG2B, bool NTL, int UF = LA_UF>
+template <int LOG2B, bool NTL, int UF = LA_UF, int JW = LA_JW>
 __device__ __forceinline__ bool la_anchor(const ProcArgs &a, int jb, int ba, unsigned char *smem) {
     if (ba < a.la_n[2]) {
-        la_anchor_far<LOG2B, 3, NTL, UF>(a, jb, ba, smem);
+        la_anchor_far<LOG2B, 3, NTL, UF, JW>(a, jb, ba, smem);
         return true;
     }
     ba -= a.la_n[2];
     if (ba < a.la_n[1]) {
-        la_anchor_far<LOG2B, 2, NTL, UF>(a, jb, ba, smem);
+        la_anchor_far<LOG2B, 2, NTL, UF, JW>(a, jb, ba, smem);
         // level-1 anchor ba after the level-2 walk: the level-2 workgroups
         // finish first (r4 timeline: 8.9 us median against 13.4 for level 3
         // and ~15 for the in-step level-1 walks they replace)
