@@ -376,8 +376,9 @@ class FFTConvolver(_Base):
         return int(lib().fftconv_uniform_far_windows(self._h))
 
     def lookahead_probe(self) -> int:
-        """(tests) post-step state-word observations of the FFTCONV_LA_PROBE
-        launches; -1 when the probe is off."""
+        """(tests) live state words the FFTCONV_LA_PROBE launches' anchors found
+        already rewritten by their own launch's steps (the anchors compute from
+        launch-start copies); -1 when the probe is off."""
         return int(lib().fftconv_uniform_lookahead_probe(self._h))
 
     def ir_spectrum(self, channel: int, segment: int) -> np.ndarray:

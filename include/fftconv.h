@@ -217,9 +217,11 @@ int fftconv_uniform_lookahead_parts(const fftconv_uniform *h);
  * calls; bit-identical to summing them every block), 0 = not used */
 int fftconv_uniform_far_windows(const fftconv_uniform *h);
 /* (tests) with FFTCONV_LA_PROBE=1 in the environment when the handle was
- * created, the lookahead launches force their anchors to observe the
- * post-step state word (la.hpp la_anchor_state): the number of such
- * observations so far; -1 when the probe is off (the default) */
+ * created, the lookahead launches make their anchors wait for the steps and
+ * read the live state words, which they do not compute from (they use the
+ * launch-start copies, la.hpp la_anchor_state): the number of live words
+ * found already rewritten by the same launch so far; -1 when the probe is
+ * off (the default) */
 int fftconv_uniform_lookahead_probe(const fftconv_uniform *h);
 size_t fftconv_uniform_block_size(const fftconv_uniform *h);   /* next_power_of_two(max_block_size) */
 size_t fftconv_uniform_seg_count(const fftconv_uniform *h);
