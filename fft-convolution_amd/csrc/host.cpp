@@ -476,7 +476,12 @@ struct UniformCore {
         a.laW = laW.p;
         a.la_c0 = (int)chan0;
         a.la_t = (int)((la_t + per - 1) % per);
+        // a rebuild of every channel also fills the next lookahead launch's
+        // copy of the state words (la_job then copies nothing)
+        const bool whole = chan0 == 0 && nch == C && lav.p;
+        if (whole) a.job[0].vnext = lav.p + (size_t)(la_seq & 1) * C;
         HIP_TRY(launch_la_rebuild(log2b, a, (int)(chan0 + nch), s));
+        if (whole) view_ok = true;
         return FFTCONV_OK;
     }
 

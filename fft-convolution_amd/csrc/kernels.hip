@@ -2941,11 +2941,18 @@ __global__ void la_rebuild_state_kernel(ProcArgs a) {
     const int c = a.la_c0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (c >= a.la_channels) return;
     const int4 st = a.job[0].state[c];
-    if (!la_eligible<LOG2B>(st, a.job[0].n)) return;
+    // (vnext, when the host passes it: the next lookahead launch's copy of
+    // every word, la.hpp la_anchor_state -- no separate refresh copy)
+    int4 *vn = a.job[0].vnext;
+    if (!la_eligible<LOG2B>(st, a.job[0].n)) {
+        if (vn) vn[c] = st;
+        return;
+    }
     int nf = st.w & ~(LA_MASK | SEQ_MASK);  // (launch tag 0: no process launch wrote it)
     // (the anchors wrote the other window of each level: toggle its flag)
     for (int lv = 1; lv <= a.la_nlv; ++lv) nf = (nf ^ la_flag_win(lv)) | la_flag_live(lv);
     a.job[0].state[c].w = nf;
+    if (vn) vn[c] = make_int4(st.x, st.y, st.z, nf);
 }
 
 template <int LOG2B>
