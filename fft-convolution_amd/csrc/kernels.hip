@@ -1766,6 +1766,12 @@ __global__ __launch_bounds__(NT) void ir_segments_kernel(IrArgs a) {
 #define FFTCONV_IR_SPW 2
 #endif
 constexpr int IR_SPW = FFTCONV_IR_SPW;
+// segments loaded ahead of the one being transformed (1: the next one only)
+#ifndef FFTCONV_IR_PF
+#define FFTCONV_IR_PF 1
+#endif
+constexpr int IR_PF = FFTCONV_IR_PF;
+static_assert(IR_PF >= 1 && IR_PF <= IR_SPW, "prefetch depth");
 template <int LOG2B>
 constexpr int ir_nw() { return LOG2B >= 7 ? 8 : 4; }
 template <int LOG2B>
@@ -1829,21 +1835,30 @@ __global__ __launch_bounds__(64 * ir_nw<LOG2B>()) void ir_segments_wave_kernel(I
         }
     };
     const int i0 = (blockIdx.x * NW + wave) * IR_SPW;
-    float2 cur[NPL], curh[NPL], nxt[NPL], nxth[NPL];
-    if (i0 < a.S && i0 < active) load(i0, cur, curh);
+    // a ring of IR_PF + 1 segments in registers: segment q + IR_PF is loaded
+    // while segment q is transformed (the loop is unrolled, so every ring
+    // index is a constant and no in-flight load is ever copied)
+    constexpr int RING = IR_PF + 1;
+    float2 rl[RING][NPL], rh[RING][NPL];
+#pragma unroll
+    for (int k = 0; k < IR_PF && k < IR_SPW; ++k)
+        if (i0 + k < a.S && i0 + k < active) load(i0 + k, rl[k], rh[k]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // (the twiddle table)
+#pragma unroll
     for (int q = 0; q < IR_SPW; ++q) {
         const int i = i0 + q;
         if (i >= a.S) break;
         float2 *row = a.H + c * rows + (size_t)i * B;
-        if (i + 1 < a.S && i + 1 < active && q + 1 < IR_SPW) load(i + 1, nxt, nxth);  // (in flight under this FFT)
+        if (q + IR_PF < IR_SPW && i + IR_PF < a.S && i + IR_PF < active)
+            load(i + IR_PF, rl[(q + IR_PF) % RING], rh[(q + IR_PF) % RING]);  // (in flight under these FFTs)
         if (i >= active) {  // :210-212
             for (int m = lane; m < B; m += 64) row[m] = make_float2(0.f, 0.f);
             continue;
         }
+        float2(&cur)[NPL] = rl[q % RING];
         if constexpr (REG) {
-            wave_stage0_padded<LOG2B>(cur, curh, bufA);
+            wave_stage0_padded<LOG2B>(cur, rh[q % RING], bufA);
             wave_sync();
             wave_r2c_post<LOG2B, 1, TwStaged<LOG2B>, true, (FFTCONV_IR_NTST != 0)>(bufA, nullptr, TwStaged<LOG2B>{twl},
                                                                                  nullptr, row);
@@ -1859,11 +1874,6 @@ __global__ __launch_bounds__(64 * ir_nw<LOG2B>()) void ir_segments_wave_kernel(I
             for (int m = lane; m < B; m += 64) row[m] = real_post<LOG2B, 64>(Z, m, twl);
         }
         wave_sync();  // (the next segment overwrites both buffers)
-#pragma unroll
-        for (int u = 0; u < NPL; ++u) {
-            cur[u] = nxt[u];
-            if constexpr (REG) curh[u] = nxth[u];
-        }
     }
 }
 
